@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X proof-of-work search (BASELINE.json metric: MD5 candidates/s, GH/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step is one batch of the hot path: every rank searches its prefix partition
+(worker_byte = rank, worker_bits = log2 N; coordinator.go:127,326) over the same
+k-window holding 2^36 candidates per GPU (nonce
+[1,2,3,4], N = 32 trailing zeros -- unreachable, so the whole window is hashed --
+in the L = 4 chunk segment k >= 2^24), followed by the batch-boundary
+all-reduce MIN of [best index, running] over RCCL.  value = candidates hashed
+by all ranks / max-over-ranks wall time of the K timed steps.
+
+Also reported: the kernel's roofline (INT32 VALU issue, measured with HIP events
+on the search stream), time-to-secret for the BASELINE configs, and the CPU
+baseline (the oracle's restatement of the reference Go loop on the host cores).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-proof-of-work_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import torch  # noqa: E402  (before libdpow: one shared HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import distpow  # noqa: E402
+from distpow.node import node_mine, partition_of_rank  # noqa: E402
+
+NONCE = [1, 2, 3, 4]
+SWEEP_NTZ = 32
+CANDIDATES_PER_GPU_PER_STEP = 1 << 36
+K0 = 1 << 24                      # start of the L = 4 segment
+OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
+# INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,
+# the MI355X_MICROARCH.md FP32 vector peak (157.3 TFLOP/s) / 2 FLOP per FMA lane-op.
+PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    wb, wbits = partition_of_rank(rank, world)
+    R = 1 << (8 - wbits)
+    batch_k = CANDIDATES_PER_GPU_PER_STEP // R  # same k-window on every rank
+
+    miner = distpow.Miner(local_rank)
+    dev = torch.device("cuda", local_rank)
+    red = torch.empty(2, dtype=torch.int64, device=dev)
+
+    def step(s):
+        k_begin = K0 + s * batch_k
+        r = miner.search(NONCE, SWEEP_NTZ, wb, wbits, k_begin, k_begin + batch_k)
+        assert r.status == distpow.EXHAUSTED, r  # N = 32 is unreachable in 2^36 candidates
+        if world > 1:
+            red[0] = r.global_idx if r.status == distpow.FOUND else distpow.DPOW_NO_HIT
+            red[1] = 1
+            dist.all_reduce(red, op=dist.ReduceOp.MIN)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for s in range(args.warmup):
+        step(s)
+    miner.reset_stats()
+    ext = torch.cuda.ExternalStream(miner.stream_handle())
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record(ext)
+    for s in range(args.warmup, args.warmup + args.steps):
+        step(s)
+    ev1.record(ext)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = miner.stats()
+    stream_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    total_candidates = world * CANDIDATES_PER_GPU_PER_STEP * args.steps
+    value = total_candidates / elapsed_max / 1e9
+    # roofline of the dominant (only) kernel: algorithmic ops per launch / avg launch duration
+    avg_launch_ms = st.kernel_ms / max(1, st.launches)
+    cand_per_launch = st.candidates / max(1, st.launches)
+    achieved_tops = cand_per_launch * OPS_PER_CANDIDATE / (avg_launch_ms * 1e-3) / 1e12
+    kernel_ghs = st.candidates / (st.kernel_ms * 1e-3) / 1e9
+
+    # time-to-secret for the BASELINE configs (deterministic answers; node-wide when world > 1)
+    tts = {}
+    ttsk = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8),
+            ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5)]
+    for nonce, n in ttsk:
+        barrier()
+        t1 = time.perf_counter()
+        res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
+                        batch_k=(1 << 26) >> (8 - wbits) if wbits else 1 << 26, device=dev)
+        barrier()
+        dt = time.perf_counter() - t1
+        assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
+        tts[f"{bytes(nonce).hex()}/{n}"] = {"ms": round(dt * 1e3, 3), "global_idx": res.global_idx,
+                                            "secret": list(res.secret)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_threads, args.cpu_seconds)
+
+    if rank == 0:
+        cus, bpc, tpb = miner.geometry()
+        out = {
+            "metric": "MD5 candidates/sec (GH/s), whole node",
+            "value": round(value, 3),
+            "unit": "GH/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {
+                "workload": "sweep: nonce [1,2,3,4], 32 trailing zeros (unreachable), 2^36 candidates per GPU "
+                            "per step in the L=4 chunk segment (k >= 2^24); per-step RCCL MIN all-reduce",
+                "nonce": NONCE, "ntz": SWEEP_NTZ, "candidates_per_gpu_per_step": CANDIDATES_PER_GPU_PER_STEP,
+                "k_window_per_step": batch_k, "parallelism": f"prefix-partition x{world} (workerBits={wbits})",
+            },
+            "per_gpu_ghs": round(value / world, 3),
+            "kernel_ghs": round(kernel_ghs, 3),
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved_tops, 3),
+                "peak": round(PEAK_TOPS, 3),
+                "unit": "TOP/s (INT32 VALU lane-ops)",
+                "frac": round(achieved_tops / PEAK_TOPS, 4),
+                "traffic": None,
+                "ops_per_candidate": OPS_PER_CANDIDATE,
+                "avg_launch_ms": round(avg_launch_ms, 4),
+                "candidates_per_launch": int(cand_per_launch),
+                "launches": int(st.launches),
+            },
+            "stream_event_ms": round(stream_ms, 3),
+            "time_to_secret": tts,
+            "cpu_baseline": cpu,
+            "geometry": {"cus": cus, "threads_per_block": tpb},
+        }
+        print(json.dumps(out), flush=True)
+    miner.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(threads, seconds):
+    """The oracle's restatement of the reference Go loop (worker.go:318-400, incl. %x formatting and the
+    trailing-'0' scan) on host cores, workerBits partitioned, bounded sample of the same workload."""
+    from _oracle import Oracle
+    o = Oracle()
+    W = o.lib.oracle_bench_workers(threads)
+    R = 256 // W
+    # calibrate on a short window, then size the sample to ~`seconds`
+    k_cal = max(1, 20000 // R)
+    secs, hashes = o.cpu_bench(NONCE, SWEEP_NTZ, W, K0, k_cal)
+    rate = hashes / secs
+    k_count = max(1, int(rate * seconds / (R * W)))
+    secs, hashes = o.cpu_bench(NONCE, SWEEP_NTZ, W, K0, k_count)
+    return {"value": round(hashes / secs / 1e9, 6), "unit": "GH/s", "cores": W, "kind": "port",
+            "sample": f"{hashes} candidates (k in [2^24, 2^24+{k_count}) x {W} workers, nonce [1,2,3,4], "
+                      f"N=32) in {secs:.2f} s; C restatement of worker.go:318-400 (oracle/dpow_oracle.c)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+// dpow_common.h -- definitions shared by the gfx950 kernels and the host planner.
+//
+// MD5 constants (RFC 1321 section 3.4) and the launch descriptor that carries
+// one launch window of the search (see DESIGN.md "Data layout").
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define DPOW_HD __host__ __device__ __forceinline__
+#else
+#define DPOW_HD inline
+#endif
+
+namespace dpow {
+
+// T[i] = floor(|sin(i+1)| * 2^32)
+constexpr uint32_t kMd5K[64] = {
+    0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+    0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+    0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+    0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+    0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+    0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+    0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+    0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+
+constexpr uint32_t kMd5IV[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+
+// Rotation of step i.
+constexpr int md5_shift(int i) {
+    return (i < 16)   ? (i % 4 == 0 ? 7 : i % 4 == 1 ? 12 : i % 4 == 2 ? 17 : 22)
+           : (i < 32) ? (i % 4 == 0 ? 5 : i % 4 == 1 ? 9 : i % 4 == 2 ? 14 : 20)
+           : (i < 48) ? (i % 4 == 0 ? 4 : i % 4 == 1 ? 11 : i % 4 == 2 ? 16 : 23)
+                      : (i % 4 == 0 ? 6 : i % 4 == 1 ? 10 : i % 4 == 2 ? 15 : 21);
+}
+
+// Message word read by step i.
+constexpr int md5_word(int i) {
+    return (i < 16) ? i : (i < 32) ? (1 + 5 * i) % 16 : (i < 48) ? (5 + 3 * i) % 16 : (7 * i) % 16;
+}
+
+// bitop3 truth tables, index = (x << 2) | (y << 1) | z.
+constexpr uint32_t kBop3F = 0xCA;  // F = x ? y : z
+constexpr uint32_t kBop3G = 0xE4;  // G = z ? x : y
+constexpr uint32_t kBop3H = 0x96;  // H = x ^ y ^ z
+constexpr uint32_t kBop3I = 0x39;  // I = y ^ (x | ~z)
+
+// Candidates per lane per wave-block (interleaved for ILP).
+#ifndef DPOW_NC
+#define DPOW_NC 2
+#endif
+constexpr int kNC = DPOW_NC;
+constexpr int kWaveBlock = 64 * kNC;  // local indices per wave-block
+constexpr int kBlockThreads = 256;    // 4 waves per workgroup
+
+// Device control block (one per context, in HBM).
+struct Ctrl {
+    unsigned long long best;  // min global index found (DPOW_NO_HIT = none), atomicMin target
+    uint32_t stop;            // set by the watcher when the host cancel flag is raised
+    uint32_t done;            // worker waves retired (cumulative within one search)
+};
+
+// One launch window.  Passed by value as the kernel argument (kernarg segment,
+// read with scalar loads).
+struct Launch {
+    uint32_t iv[4];        // chaining value entering the first final block (midstate)
+    uint32_t T[32];        // final block(s) template words, variable bytes zeroed
+    uint32_t KT[128];      // K[s] + T[16 b + word(s)] for every step s of block b
+    uint64_t i_begin;      // local index range [i_begin, i_end)
+    uint64_t i_end;
+    uint64_t wb_begin;     // i_begin rounded down to 64
+    uint64_t n_wblocks;    // wave-blocks covering [wb_begin, i_end)
+    uint32_t rbits;        // R = 1 << rbits threadBytes per k
+    uint32_t base_tb;      // uint8(worker_byte << rbits)
+    uint32_t dmask;        // mask on the final D word for min(ntz, 8) trailing nibbles
+    uint32_t ntz;          // requested trailing zeros (full digest check when > 8)
+    uint32_t done_target;  // watcher exits when Ctrl::done reaches this
+    uint32_t iters;        // wave-blocks per worker wave (contiguous run)
+    Ctrl *ctrl;
+    const uint32_t *cancel;  // device-visible alias of the pinned host cancel flag
+};
+
+// Nibble positions (bit offsets) of a digest word in hex-string order from the
+// end: the last hex character is the low nibble of the word's top byte.
+DPOW_HD uint32_t tail_nibble_mask(uint32_t n) {
+    const uint32_t pos[8] = {24, 28, 16, 20, 8, 12, 0, 4};
+    uint32_t m = 0;
+    for (uint32_t j = 0; j < n && j < 8; ++j) m |= 0xFu << pos[j];
+    return m;
+}
+
+DPOW_HD uint32_t bswap32(uint32_t x) {
+    return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
+}
+
+// Trailing '0' hex characters of the digest (A,B,C,D little-endian words):
+// the hex string is the 128-bit big-endian number bswap(A)|bswap(B)|bswap(C)|bswap(D).
+DPOW_HD uint32_t trailing_zero_nibbles(uint32_t A, uint32_t B, uint32_t C, uint32_t D) {
+    const uint32_t w[4] = {bswap32(D), bswap32(C), bswap32(B), bswap32(A)};
+    uint32_t n = 0;
+    for (int j = 0; j < 4; ++j) {
+        if (w[j] == 0) { n += 8; continue; }
+        uint32_t x = w[j];
+        while ((x & 0xF) == 0) { x >>= 4; ++n; }
+        break;
+    }
+    return n;
+}
+
+// Lane arithmetic shared by the kernel and the host emulation
+// (dpow_plan_candidate): the variable 4 bytes V = threadByte | (k mod 2^24) << 8
+// of local index i = i0 + lane, i0 a multiple of 64, split into a wave-uniform
+// part and a per-lane constant.
+DPOW_HD uint32_t lane_offset(uint32_t rbits, uint32_t lane) {
+    return rbits >= 6 ? lane : ((lane & ((1u << rbits) - 1u)) | ((lane >> rbits) << 8));
+}
+DPOW_HD uint32_t wave_uniform_v(uint64_t i0, uint32_t rbits, uint32_t base_tb) {
+    const uint64_t R = 1ull << rbits;
+    return base_tb | (uint32_t)(i0 & (R - 1)) | ((uint32_t)((i0 >> rbits) & 0xFFFFFFu) << 8);
+}
+// Global index g = k * 256 + threadByte of a local index.
+DPOW_HD uint64_t global_of_local(uint64_t i, uint32_t rbits, uint32_t base_tb) {
+    const uint64_t R = 1ull << rbits;
+    return ((i >> rbits) << 8) | (uint64_t)(base_tb | (uint32_t)(i & (R - 1)));
+}
+
+}  // namespace dpow

@@ -1,0 +1,198 @@
+// md5_search.hip -- the gfx950 proof-of-work search kernel.
+//
+// Replaces the reference miner's inner loop (worker.go:318-400): for every
+// candidate threadByte || chunk_k of the worker partition, MD5(nonce || it) and
+// the trailing-'0' test of its hex form.  Pure INT32 VALU work: each lane runs
+// an unrolled, register-resident MD5 of the final message block(s) of kNC
+// candidates (interleaved for ILP), the message words being wave-uniform
+// (kernel arguments, SGPRs) except the 4 bytes threadByte | k_lo << 8.
+//
+// Work decomposition: local index i = k * R + t (the reference's order, k outer,
+// t inner).  A wave-block is 64 * kNC consecutive indices (lane l, slot j ->
+// i0 + 64 j + l).  Worker waves walk wave-blocks grid-stride in increasing
+// order; the first hit of a wave-block (lowest slot, then lowest lane) goes to
+// atomicMin on the global index g = k * 256 + threadByte, which is monotone in
+// i, so the minimum is the reference's first hit.  A wave stops at the first
+// wave-block whose first index is >= the current minimum, so every candidate
+// below the answer is evaluated and the result is deterministic.
+//
+// Workgroup 0 of the grid is a watcher: one lane polls the pinned host
+// cancel flag (Found/Cancel, worker.go:194,209) and raises Ctrl::stop, which
+// every worker wave reads once per wave-block together with Ctrl::best.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dpow_common.h"
+
+namespace dpow {
+
+#define DPOW_DEV __device__ __forceinline__
+
+template <int I>
+DPOW_DEV uint32_t md5_fn(uint32_t x, uint32_t y, uint32_t z) {
+    constexpr int r = I / 16;
+    constexpr uint32_t tt = r == 0 ? kBop3F : r == 1 ? kBop3G : r == 2 ? kBop3H : kBop3I;
+    return __builtin_amdgcn_bitop3_b32(x, y, z, tt);
+}
+
+// Per-candidate variable message parts.
+struct VarWords {
+    uint32_t lo_s[kNC];  // wave-uniform part of V << 8*SH (word W0)
+    uint32_t lo_v;       // per-lane part of V << 8*SH (the same for every slot)
+    uint32_t hi[kNC];    // V >> (32 - 8*SH), added for steps reading word W0+1
+};
+
+template <int NBLK, int W0, int SH, int BLK, int I, int NCAND>
+DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
+    if constexpr (I < 64) {
+        constexpr int ai = (64 - I) % 4, bi = (ai + 1) % 4, ci = (ai + 2) % 4, di = (ai + 3) % 4;
+        constexpr int m = 16 * BLK + md5_word(I);
+        constexpr int s = md5_shift(I);
+        const uint32_t kt = L.KT[64 * BLK + I];
+#pragma unroll
+        for (int j = 0; j < NCAND; ++j) {
+            uint32_t km = kt;
+            if constexpr (m == W0) km = (km + v.lo_s[j]) + v.lo_v;
+            if constexpr (SH != 0 && m == W0 + 1) km += v.hi[j];
+            const uint32_t f = md5_fn<I>(x[bi][j], x[ci][j], x[di][j]);
+            x[ai][j] = x[bi][j] + __builtin_rotateleft32(x[ai][j] + f + km, s);
+        }
+        md5_steps<NBLK, W0, SH, BLK, I + 1, NCAND>(x, L, v);
+    }
+}
+
+// Final-block compression(s) of NCAND candidates; returns the digest words.
+template <int NBLK, int W0, int SH, int NCAND>
+DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords &v) {
+    uint32_t x[4][kNC];
+#pragma unroll
+    for (int j = 0; j < NCAND; ++j) {
+        x[0][j] = L.iv[0]; x[1][j] = L.iv[1]; x[2][j] = L.iv[2]; x[3][j] = L.iv[3];
+    }
+    md5_steps<NBLK, W0, SH, 0, 0, NCAND>(x, L, v);
+#pragma unroll
+    for (int j = 0; j < NCAND; ++j)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) out[w][j] = L.iv[w] + x[w][j];
+    if constexpr (NBLK == 2) {
+#pragma unroll
+        for (int j = 0; j < NCAND; ++j)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) x[w][j] = out[w][j];
+        md5_steps<NBLK, W0, SH, 1, 0, NCAND>(x, L, v);
+#pragma unroll
+        for (int j = 0; j < NCAND; ++j)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) out[w][j] += x[w][j];
+    }
+}
+
+template <int SH>
+DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff) {
+    v.lo_s[j] = vs << (8 * SH);
+    v.lo_v = loff << (8 * SH);
+    if constexpr (SH != 0) v.hi[j] = (vs + loff) >> (32 - 8 * SH);
+    else v.hi[j] = 0;
+}
+
+// Full digest test of one lane's candidate (rare path: only when the D-word
+// test passed and ntz > 8, i.e. probability 2^-32 per candidate).
+template <int NBLK, int W0, int SH>
+DPOW_DEV bool full_check(const Launch &L, uint32_t vs, uint32_t loff) {
+    VarWords v;
+    var_words<SH>(v, 0, vs, loff);
+    uint32_t out[4][kNC];
+    md5_tail<NBLK, W0, SH, 1>(out, L, v);
+    return trailing_zero_nibbles(out[0][0], out[1][0], out[2][0], out[3][0]) >= L.ntz;
+}
+
+DPOW_DEV void watcher(const Launch &L) {
+    if (threadIdx.x != 0) return;
+    for (;;) {
+        const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done >= L.done_target) return;
+        if (__hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+            __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(32);
+    }
+}
+
+DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
+    lo = lo < 0 ? 0 : (lo > 64 ? 64 : lo);
+    hi = hi < 0 ? 0 : (hi > 64 ? 64 : hi);
+    if (hi <= lo) return 0;
+    const uint64_t upto_hi = hi == 64 ? ~0ull : ((1ull << hi) - 1ull);
+    const uint64_t below_lo = lo == 64 ? ~0ull : ((1ull << lo) - 1ull);
+    return upto_hi & ~below_lo;
+}
+
+template <int NBLK, int W0, int SH>
+__global__ void __launch_bounds__(kBlockThreads) md5_search_kernel(const Launch L) {
+    constexpr uint32_t wpb = kBlockThreads / 64;
+    if (blockIdx.x == 0) {  // dispatched first: the watcher
+        watcher(L);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    // Worker wave w owns the contiguous run of wave-blocks [w * iters, (w + 1) * iters).
+    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x - 1) * wpb + (threadIdx.x >> 6));
+    const uint64_t b_begin = (uint64_t)wave * L.iters;
+    const uint64_t b_end = b_begin + L.iters < L.n_wblocks ? b_begin + L.iters : L.n_wblocks;
+    const uint32_t loff = lane_offset(L.rbits, lane);
+
+    unsigned long long best = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t stop = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+        const uint64_t i0 = L.wb_begin + b * (uint64_t)kWaveBlock;
+        const uint64_t ifirst = i0 < L.i_begin ? L.i_begin : i0;
+        if (stop != 0u || global_of_local(ifirst, L.rbits, L.base_tb) >= best) break;
+        // Issued now, consumed at the next wave-block: the load latency hides
+        // behind this wave-block's ~kNC*250 VALU instructions.
+        const unsigned long long best_next =
+            __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t stop_next = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+        uint32_t vs[kNC];
+        VarWords v;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+            vs[j] = wave_uniform_v(i0 + 64u * j, L.rbits, L.base_tb);
+            var_words<SH>(v, j, vs[j], loff);
+        }
+        uint32_t dig[4][kNC];
+        md5_tail<NBLK, W0, SH, kNC>(dig, L, v);
+
+        uint64_t bal[kNC];
+        uint64_t any = 0;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+            bal[j] = __ballot((dig[3][j] & L.dmask) == 0u);
+            any |= bal[j];
+        }
+        if (any != 0) {
+#pragma unroll
+            for (int j = 0; j < kNC; ++j) {
+                const uint64_t ij = i0 + 64u * j;
+                uint64_t m = bal[j] & lane_range_mask((int64_t)(L.i_begin - ij), (int64_t)(L.i_end - ij));
+                if (m != 0 && L.ntz > 8u) {
+                    const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, vs[j], loff);
+                    m = __ballot(ok);
+                }
+                if (m != 0) {
+                    const uint64_t g = global_of_local(ij + (uint64_t)__builtin_ctzll(m), L.rbits, L.base_tb);
+                    if (lane == 0) atomicMin(&L.ctrl->best, (unsigned long long)g);
+                    if (g < best) best = g;
+                    break;
+                }
+            }
+        }
+        best = best_next < best ? best_next : best;
+        stop = stop_next;
+    }
+    if (lane == 0) __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace dpow

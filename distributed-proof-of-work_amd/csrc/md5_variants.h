@@ -1,0 +1,34 @@
+// md5_variants.h -- per-(NBLK, SH) launch entry points (defined in md5_variant.hip)
+// and the dispatcher over them (md5_dispatch.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dpow_common.h"
+
+namespace dpow {
+
+#define DPOW_DECL_VARIANT(n, s)                                                                  \
+    hipError_t variant_launch_##n##_##s(int w0, const Launch &L, uint32_t grid, hipStream_t st); \
+    hipError_t variant_occupancy_##n##_##s(int w0, int *blocks_per_cu);
+DPOW_DECL_VARIANT(1, 0)
+DPOW_DECL_VARIANT(1, 1)
+DPOW_DECL_VARIANT(1, 2)
+DPOW_DECL_VARIANT(1, 3)
+DPOW_DECL_VARIANT(2, 0)
+DPOW_DECL_VARIANT(2, 1)
+DPOW_DECL_VARIANT(2, 2)
+DPOW_DECL_VARIANT(2, 3)
+#undef DPOW_DECL_VARIANT
+
+// True when a kernel variant exists for (nblk, w0, sh).
+inline bool variant_exists(int nblk, int w0, int sh) {
+    if (sh < 0 || sh > 3) return false;
+    if (nblk == 1) return w0 >= 0 && w0 <= 13;
+    if (nblk == 2) return w0 >= 12 && w0 <= 15;
+    return false;
+}
+
+hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream);
+hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu);
+
+}  // namespace dpow

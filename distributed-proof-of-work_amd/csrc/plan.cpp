@@ -1,0 +1,116 @@
+// plan.cpp -- host planning of a search window into kernel launches.
+//
+// The reference enumerates, per worker partition (worker.go:301-316),
+//   for k = 0, 1, ... (chunk_k = nextChunk^k([]), worker.go:234-244, 399)
+//     for t in 0..R-1: msg = nonce || threadByte[t] || chunk_k   (worker.go:319-353)
+// A launch covers a k-range in which the message layout is uniform:
+//   * the chunk length L is constant (segment boundaries k = 1, 2^8, 2^16, 2^24, 2^32),
+//   * for L >= 4 the bytes of k above the low 24 bits are constant (split at multiples of 2^24),
+// so the only per-candidate bytes are V = threadByte | (k mod 2^24) << 8, at byte
+// offset p = nonce_len mod 64 of the first final block.  Whole nonce-only
+// blocks before it are hashed here once (midstate).
+#include "plan.h"
+
+#include <string.h>
+
+#include "md5_host.h"
+
+namespace dpow {
+
+uint32_t chunk_len_of(uint64_t k) {
+    uint32_t n = 0;
+    while (k) { ++n; k >>= 8; }
+    return n;
+}
+
+uint64_t segment_end(uint64_t k) {
+    const uint32_t L = chunk_len_of(k);
+    if (L == 0) return 1;
+    if (L <= 3) return 1ull << (8 * L);
+    return ((k >> 24) + 1) << 24;
+}
+
+uint32_t remainder_bits(uint32_t worker_bits) { return 8u - (worker_bits % 9u); }
+
+uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits) {
+    // uint8((int(WorkerByte) << remainderBits) | i) with i = 0 (worker.go:315)
+    return (uint32_t)((worker_byte << remainder_bits(worker_bits)) & 0xFFu);
+}
+
+int plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
+                uint32_t worker_bits, uint64_t k_begin, uint64_t k_end, std::vector<PlannedLaunch> &out) {
+    out.clear();
+    if (nonce_len && !nonce) return -1;
+    if (worker_byte > 255u) return -1;
+    if (k_begin >= k_end) return 0;
+    if (k_end > (1ull << 40)) return -4;
+    const uint32_t rbits = remainder_bits(worker_bits);
+    const uint32_t base_tb = base_thread_byte(worker_byte, worker_bits);
+    const size_t blk_v = nonce_len / 64;  // first block holding variable bytes
+    const uint32_t p = (uint32_t)(nonce_len % 64);
+
+    // Midstate over nonce-only blocks.
+    uint32_t iv[4] = {kMd5IV[0], kMd5IV[1], kMd5IV[2], kMd5IV[3]};
+    for (size_t b = 0; b < blk_v; ++b) {
+        uint32_t M[16];
+        for (int w = 0; w < 16; ++w) M[w] = load_le32(nonce + 64 * b + 4 * w);
+        md5_compress(iv, M);
+    }
+
+    uint64_t k = k_begin;
+    while (k < k_end) {
+        const uint64_t ke = segment_end(k) < k_end ? segment_end(k) : k_end;
+        const uint32_t L = chunk_len_of(k);
+        const size_t msg_len = nonce_len + 1 + L;
+        const size_t total_blocks = (msg_len + 8) / 64 + 1;
+        const uint32_t nblk = (uint32_t)(total_blocks - blk_v);
+        PlannedLaunch pl;
+        memset(&pl, 0, sizeof pl);
+        Launch &Lh = pl.L;
+        uint8_t buf[128];
+        memset(buf, 0, sizeof buf);
+        if (p) memcpy(buf, nonce + 64 * blk_v, p);
+        // buf[p] = threadByte and buf[p+1 .. p+min(L,3)] = low chunk bytes: variable (left 0).
+        for (uint32_t j = 3; j < L; ++j) buf[p + 1 + j] = (uint8_t)(k >> (8 * j));
+        buf[p + 1 + L] = 0x80;
+        const uint64_t bits = (uint64_t)msg_len * 8u;
+        for (int j = 0; j < 8; ++j) buf[64 * nblk - 8 + j] = (uint8_t)(bits >> (8 * j));
+        for (int w = 0; w < 4; ++w) Lh.iv[w] = iv[w];
+        for (uint32_t w = 0; w < 16 * nblk; ++w) Lh.T[w] = load_le32(buf + 4 * w);
+        for (uint32_t b = 0; b < nblk; ++b)
+            for (int s = 0; s < 64; ++s) Lh.KT[64 * b + s] = kMd5K[s] + Lh.T[16 * b + md5_word(s)];
+        Lh.i_begin = k << rbits;
+        Lh.i_end = ke << rbits;
+        Lh.wb_begin = Lh.i_begin & ~63ull;
+        Lh.n_wblocks = (Lh.i_end - Lh.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
+        Lh.rbits = rbits;
+        Lh.base_tb = base_tb;
+        Lh.dmask = tail_nibble_mask(ntz < 8 ? ntz : 8);
+        Lh.ntz = ntz;
+        pl.info.k_begin = k;
+        pl.info.k_end = ke;
+        pl.info.i_begin = Lh.i_begin;
+        pl.info.i_end = Lh.i_end;
+        pl.info.nblk = nblk;
+        pl.info.w0 = p / 4;
+        pl.info.sh = p % 4;
+        pl.info.chunk_len = L;
+        out.push_back(pl);
+        k = ke;
+    }
+    return (int)out.size();
+}
+
+// Words of one candidate, assembled as the kernel does (wave-uniform V + lane offset).
+void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words[32]) {
+    const Launch &Lh = pl.L;
+    for (uint32_t w = 0; w < 16 * pl.info.nblk; ++w) words[w] = Lh.T[w];
+    const uint64_t i0 = local_idx & ~63ull;
+    const uint32_t lane = (uint32_t)(local_idx & 63u);
+    const uint32_t V = wave_uniform_v(i0, Lh.rbits, Lh.base_tb) + lane_offset(Lh.rbits, lane);
+    const uint32_t sh = pl.info.sh, w0 = pl.info.w0;
+    words[w0] += V << (8 * sh);
+    if (sh) words[w0 + 1] += V >> (32 - 8 * sh);
+}
+
+}  // namespace dpow

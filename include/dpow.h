@@ -1,0 +1,154 @@
+/*
+ * dpow.h -- C ABI of the MI355X proof-of-work search (libdpow.so).
+ *
+ * The drop-in boundary for philipjesic/Distributed-Proof-Of-Work's hot path:
+ * the worker's brute-force search, `miner` (worker.go:258-401), whose search
+ * loop (worker.go:301-400) is replaced by GPU dispatch.  The reference has no
+ * FFI of its own; these entry points are what its Go worker would bind through
+ * cgo (see INTEGRATION.md for the binding a maintainer would add).
+ *
+ * Plain C types only (pointers + sizes); no HIP / torch types cross the ABI.
+ * Ownership: the caller owns every host buffer passed in or out; the library
+ * owns all device memory and the pinned cancel flag of a context.
+ * Threading: one search in flight per context (the caller serialises); the
+ * cancel flag may be written from any thread while a search runs.
+ * Errors are returned as negative codes; nothing longjmps, throws or aborts.
+ */
+#ifndef DPOW_H
+#define DPOW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPOW_ABI_VERSION 1
+
+/* "no hit" sentinel for global indices: INT64_MAX, so that signed (RCCL/gloo
+ * int64 MIN) and unsigned (device atomicMin u64) reductions agree. */
+#define DPOW_NO_HIT 0x7FFFFFFFFFFFFFFFull
+
+/* Longest secret the search can return: 1 thread byte + 5 chunk bytes
+ * (k < 2^40).  Buffers are sized 16 for headroom. */
+#define DPOW_MAX_SECRET 16
+
+/* k (the number of nextChunk applications, worker.go:234-244/399) is limited to
+ * k < DPOW_K_LIMIT, i.e. chunks of at most 5 bytes (2^48 candidates). */
+#define DPOW_K_LIMIT (1ull << 40)
+
+/* dpow_search return codes */
+#define DPOW_EXHAUSTED 0   /* window searched, no hit (the reference keeps looping) */
+#define DPOW_FOUND 1       /* hit; *best_global_idx / secret filled, MD5 re-verified on host */
+#define DPOW_CANCELLED 2   /* the cancel flag was raised (Found/Cancel RPC, worker.go:194,209) */
+#define DPOW_EINVAL (-1)   /* bad argument */
+#define DPOW_EHIP (-2)     /* HIP runtime error (see dpow_last_error) */
+#define DPOW_EVERIFY (-3)  /* kernel hit failed host MD5 re-verification (never expected) */
+#define DPOW_ERANGE (-4)   /* k window beyond DPOW_K_LIMIT */
+#define DPOW_ENOMEM (-5)
+
+typedef struct dpow_ctx dpow_ctx;
+
+/* ---------------------------------------------------------------------------
+ * Context: one per GPU.  Owns persistent device buffers (control block), the
+ * HIP stream the kernels run on, and a pinned host-coherent cancel flag.
+ * Replaces the per-task setup of worker.go:301-316 (buffers + threadBytes).
+ * ------------------------------------------------------------------------- */
+int dpow_open(int device, dpow_ctx **out);
+void dpow_close(dpow_ctx *ctx);
+
+/* Pinned, host-coherent cancel flag polled by the running kernel.  Writing a
+ * non-zero value stops the search mid-launch (dpow_search returns
+ * DPOW_CANCELLED).  Replaces the per-candidate `select` on killChan
+ * (worker.go:320-345) and the writes at worker.go:194 (Cancel) / 209 (Found).
+ * The caller clears it (writes 0) before the next task. */
+volatile uint32_t *dpow_cancel_flag(dpow_ctx *ctx);
+
+/* ---------------------------------------------------------------------------
+ * The hot path.  Replaces worker.go:301-400 (the miner's enumeration loop).
+ *
+ * Searches the worker partition (worker_byte, worker_bits) -- threadBytes
+ * uint8((worker_byte << R_bits) | t), R_bits = 8 - worker_bits % 9
+ * (worker.go:302-316) -- over chunks k in [k_begin, k_end) (chunk_k = the
+ * minimal little-endian bytes of k, i.e. nextChunk applied k times), in the
+ * reference's order (k outer, t inner), for the first candidate whose
+ * hex(MD5(nonce || threadByte || chunk_k)) ends in `ntz` '0' characters
+ * (worker.go:353-356, hasNumZeroesSuffix worker.go:246-256).
+ *
+ * best_global_idx (in/out): on input an upper bound (DPOW_NO_HIT = none); only
+ * hits with global index below it are reported.  Global index
+ * g = k * 256 + threadByte; it is monotone in the worker's local order, so the
+ * minimum over partitions equals the worker_bits = 0 answer.
+ * On DPOW_FOUND, secret_out[0..*secret_len) = threadByte || chunk_k (the
+ * `Secret` of WorkerResult, worker.go:357-362), recomputed and verified with
+ * a host MD5 before returning.
+ * ------------------------------------------------------------------------- */
+int dpow_search(dpow_ctx *ctx, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,
+                uint32_t worker_byte, uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,
+                uint64_t *best_global_idx, uint8_t secret_out[DPOW_MAX_SECRET],
+                size_t *secret_len);
+
+/* ---------------------------------------------------------------------------
+ * Host helpers (no GPU needed).
+ * ------------------------------------------------------------------------- */
+/* Secret bytes of a global index: threadByte = g & 255, chunk = minimal LE bytes of g >> 8. */
+int dpow_secret_from_index(uint64_t global_idx, uint8_t secret_out[DPOW_MAX_SECRET],
+                           size_t *secret_len);
+/* Host MD5 (RFC 1321) of msg -> 16-byte digest. */
+void dpow_md5(const uint8_t *msg, size_t len, uint8_t digest_out[16]);
+/* Number of trailing '0' characters of the 32-char hex form of a digest. */
+uint32_t dpow_trailing_zero_nibbles(const uint8_t digest[16]);
+/* 1 if hex(MD5(nonce || secret)) ends in >= ntz '0' characters, else 0. */
+int dpow_verify(const uint8_t *nonce, size_t nonce_len, const uint8_t *secret,
+                size_t secret_len, uint32_t ntz);
+
+/* Launch plan of a window (host logic of dpow_search, exposed for testing):
+ * one entry per kernel launch.  Returns the number of launches (may exceed
+ * max_launches, in which case only the first max_launches are written), or a
+ * negative error code. */
+typedef struct dpow_plan_launch {
+    uint64_t k_begin, k_end;   /* chunk range of this launch */
+    uint64_t i_begin, i_end;   /* local index range (k * R + t) */
+    uint32_t nblk;             /* final MD5 blocks computed per candidate (1 or 2) */
+    uint32_t w0, sh;           /* variable bytes start at word w0, byte shift sh */
+    uint32_t chunk_len;        /* L: chunk bytes for every k of this launch */
+} dpow_plan_launch;
+int dpow_plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte,
+                     uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,
+                     dpow_plan_launch *out, size_t max_launches);
+
+/* Final-block message words and chaining value the kernel hashes for local
+ * index `local_idx` of a partition, assembled with the same template + lane
+ * arithmetic the kernel uses.  words_out: 16 * (*nblk_out) words. */
+int dpow_plan_candidate(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte,
+                        uint32_t worker_bits, uint64_t local_idx, uint32_t iv_out[4],
+                        uint32_t words_out[32], uint32_t *nblk_out);
+
+/* ---------------------------------------------------------------------------
+ * Introspection / measurement.
+ * ------------------------------------------------------------------------- */
+typedef struct dpow_stats {
+    uint64_t searches;     /* dpow_search calls */
+    uint64_t launches;     /* kernel launches */
+    uint64_t candidates;   /* candidates covered by the launched windows */
+    double kernel_ms;      /* sum of per-launch HIP-event durations on the ctx stream */
+} dpow_stats;
+int dpow_get_stats(dpow_ctx *ctx, dpow_stats *out);
+void dpow_reset_stats(dpow_ctx *ctx);
+/* The hipStream_t the context's kernels run on (as void*, for event timing). */
+void *dpow_stream(dpow_ctx *ctx);
+/* Device ordinal of the context. */
+int dpow_device(dpow_ctx *ctx);
+/* Worker waves per launch and CUs used (for reporting). */
+int dpow_geometry(dpow_ctx *ctx, uint32_t *cus, uint32_t *blocks_per_cu, uint32_t *threads_per_block);
+/* Thread-local description of the last error. */
+const char *dpow_last_error(void);
+int dpow_abi_version(void);
+/* Number of visible HIP devices (0 when none; never an error). */
+int dpow_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPOW_H */

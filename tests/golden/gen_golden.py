@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/pow_golden.json -- golden vectors for the proof-of-work search.
+
+TEST INFRASTRUCTURE.  The reference (philipjesic/Distributed-Proof-Of-Work) is Go,
+ships no tests or fixtures, and there is no Go toolchain in this image, so its
+outputs cannot be produced by running it.  The vectors here come from
+
+  * an independent pure-Python restatement of the reference's miner loop
+    (worker.go:234-244 nextChunk, 246-256 hasNumZeroesSuffix, 301-400 miner),
+    using hashlib.md5 (OpenSSL, RFC 1321) and '%x' formatting via bytes.hex();
+  * for the two big cases (N=7, N=8: 2.3e8 / 4.1e9 candidates) the C oracle in
+    oracle/ (built separately), run over contiguous k sub-windows in parallel
+    threads; the first sub-window with a hit is the sequential answer.  Its
+    small-case answers are cross-checked against the Python restatement first.
+
+Every case is also checked against SURVEY.md Appendix A where the survey lists it.
+
+Usage:  python tests/golden/gen_golden.py [--big]
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+
+RFC1321_SUITE = [  # RFC 1321 Appendix A.5
+    ("", "d41d8cd98f00b204e9800998ecf8427e"),
+    ("a", "0cc175b9c0f1b6a831c399e269772661"),
+    ("abc", "900150983cd24fb0d6963f7d28e17f72"),
+    ("message digest", "f96b697d7cb7938d525a2f31aaf161d0"),
+    ("abcdefghijklmnopqrstuvwxyz", "c3fcd3d76192e4007dfb496cca67e13b"),
+    ("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789",
+     "d174ab98d277d9f5a5611c2c9f419d9f"),
+    ("1234567890" * 8, "57edf4a22be3c955ac49da2e2107b67a"),
+]
+
+# SURVEY.md Appendix A (computed by the survey in this container).
+SURVEY_APPENDIX_A = {
+    ((1, 2, 3, 4), 0): ([0], 0),
+    ((1, 2, 3, 4), 1): ([3], 3),
+    ((1, 2, 3, 4), 2): ([97], 97),
+    ((1, 2, 3, 4), 3): ([97], 97),
+    ((1, 2, 3, 4), 4): ([116, 20], 5236),
+    ((1, 2, 3, 4), 5): ([149, 103, 2], 157589),
+    ((1, 2, 3, 4), 6): ([188, 163, 38], 2532284),
+    ((1, 2, 3, 4), 7): ([194, 170, 210, 13], 231910082),
+    ((1, 2, 3, 4), 8): ([10, 189, 80, 242], 4065377546),
+    ((5, 6, 7, 8), 5): ([84, 244, 3], 259156),
+    ((2, 2, 2, 2), 5): ([48, 119], 30512),
+    ((2, 2, 2, 2), 7): ([218, 55, 128, 17], 293615578),
+    ((2, 2, 2, 2), 8): ([218, 55, 128, 17], 293615578),
+}
+
+
+# ---------------- pure-Python restatement of worker.go ----------------
+def next_chunk(chunk):
+    """worker.go:234-244 (mutates and returns the list, like the Go slice)."""
+    for i in range(len(chunk)):
+        if chunk[i] == 0xFF:
+            chunk[i] = 0
+        else:
+            chunk[i] += 1
+            return chunk
+    chunk.append(1)
+    return chunk
+
+
+def has_num_zeroes_suffix(s, n):
+    """worker.go:246-256."""
+    found = 0
+    for ch in reversed(s):
+        if ch == "0":
+            found += 1
+        else:
+            break
+    return found >= n
+
+
+def thread_bytes(worker_byte, worker_bits):
+    """worker.go:302-316."""
+    rbits = 8 - (worker_bits % 9)
+    return [((worker_byte << rbits) | i) & 0xFF for i in range(1 << rbits)]
+
+
+def chunk_of(k):
+    out = []
+    while k:
+        out.append(k & 0xFF)
+        k >>= 8
+    return out
+
+
+def py_mine(nonce, ntz, worker_byte=0, worker_bits=0, k_begin=0, k_end=None):
+    """worker.go:301-400 over k in [k_begin, k_end). Returns (secret, global, local) or None."""
+    tbs = thread_bytes(worker_byte, worker_bits)
+    R = len(tbs)
+    chunk = chunk_of(k_begin)
+    k = k_begin
+    nb = bytes(nonce)
+    while k_end is None or k < k_end:
+        cb = bytes(chunk)
+        for t, tb in enumerate(tbs):
+            h = hashlib.md5(nb + bytes([tb]) + cb).hexdigest()  # fmt "%x"
+            if has_num_zeroes_suffix(h, ntz):
+                return [tb] + list(chunk), k * 256 + tb, k * R + t
+        chunk = next_chunk(chunk)
+        k += 1
+    return None
+
+
+def md5hex(nonce, secret):
+    return hashlib.md5(bytes(nonce) + bytes(secret)).hexdigest()
+
+
+# ---------------- C oracle driver for the big cases ----------------
+def load_oracle():
+    path = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+    lib = ctypes.CDLL(path)
+    lib.oracle_mine_window.restype = ctypes.c_int
+    lib.oracle_mine_window.argtypes = [
+        ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint8, ctypes.c_uint,
+        ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p, ctypes.POINTER(ctypes.c_size_t),
+        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    return lib
+
+
+def c_mine(lib, nonce, ntz, wb, wbits, k0, k1):
+    sec = ctypes.create_string_buffer(32)
+    slen = ctypes.c_size_t()
+    g = ctypes.c_uint64()
+    loc = ctypes.c_uint64()
+    r = lib.oracle_mine_window(bytes(nonce), len(nonce), ntz, wb, wbits, k0, k1, sec,
+                               ctypes.byref(slen), ctypes.byref(g), ctypes.byref(loc))
+    if r != 1:
+        return None
+    return list(sec.raw[:slen.value]), g.value, loc.value
+
+
+def c_mine_parallel(lib, nonce, ntz, k_end, nthreads=8, span=1 << 19):
+    """Sequential answer over k in [0, k_end) using contiguous sub-windows in threads."""
+    k0 = 0
+    while k0 < k_end:
+        wins = []
+        for j in range(nthreads):
+            a = k0 + j * span
+            b = min(k_end, a + span)
+            if a < b:
+                wins.append((a, b))
+        res = [None] * len(wins)
+
+        def run(i, a, b):
+            res[i] = c_mine(lib, nonce, ntz, 0, 0, a, b)
+
+        ths = [threading.Thread(target=run, args=(i, a, b)) for i, (a, b) in enumerate(wins)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        for r in res:
+            if r is not None:
+                return r
+        k0 = wins[-1][1]
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true", help="also compute N=7/8 cases via the C oracle")
+    args = ap.parse_args()
+
+    out = {"rfc1321": [{"msg_hex": m.encode().hex(), "md5": d} for m, d in RFC1321_SUITE],
+           "first_hits": [], "partitions": [], "windows": [], "nonce_lengths": []}
+    for m, d in RFC1321_SUITE:
+        assert hashlib.md5(m.encode()).hexdigest() == d
+
+    # 1) first hits, workerBits = 0 (the deterministic answer)
+    small = [((1, 2, 3, 4), n) for n in range(0, 7)] + [((5, 6, 7, 8), 5), ((2, 2, 2, 2), 5),
+                                                       ((5, 6, 7, 8), 3), ((9, 9, 9, 9), 4),
+                                                       ((0, 0, 0, 0), 4), ((255, 255, 255, 255), 4)]
+    for nonce, n in small:
+        secret, g, loc = py_mine(nonce, n)
+        exp = SURVEY_APPENDIX_A.get((nonce, n))
+        if exp is not None:
+            assert (secret, g) == (exp[0], exp[1]), (nonce, n, secret, g, exp)
+        out["first_hits"].append({"nonce": list(nonce), "ntz": n, "secret": secret, "global_idx": g,
+                                  "md5": md5hex(nonce, secret), "source": "python"})
+        print("first hit", nonce, n, secret, g, file=sys.stderr)
+
+    # 2) per-partition first hits (worker_byte, worker_bits) -> the multi-GPU min rule
+    for wbits in (1, 2, 3):
+        for n in (1, 2, 3, 4, 5):
+            for wb in range(1 << wbits):
+                secret, g, loc = py_mine((1, 2, 3, 4), n, wb, wbits)
+                out["partitions"].append({"nonce": [1, 2, 3, 4], "ntz": n, "worker_byte": wb,
+                                          "worker_bits": wbits, "secret": secret, "global_idx": g,
+                                          "local_idx": loc})
+    # quirks: non-power-of-two worker counts (coordinator.go:326 floor(log2 W)), wbits % 9
+    for wb, wbits in ((2, 1), (5, 2), (3, 9), (1, 10), (7, 8)):
+        secret, g, loc = py_mine((1, 2, 3, 4), 3, wb, wbits)
+        out["partitions"].append({"nonce": [1, 2, 3, 4], "ntz": 3, "worker_byte": wb,
+                                  "worker_bits": wbits, "secret": secret, "global_idx": g,
+                                  "local_idx": loc})
+
+    # 3) windows starting at chunk-length (segment) boundaries
+    for k0 in (0, 1, 255, 256, 65535, 65536, (1 << 24) - 1, 1 << 24, (1 << 24) + 12345,
+               (1 << 32) - 1, 1 << 32):
+        for n in (1, 2, 3):
+            for wbits, wb in ((0, 0), (2, 3), (3, 5)):
+                r = py_mine((1, 2, 3, 4), n, wb, wbits, k_begin=k0, k_end=k0 + 4096)
+                secret, g, loc = r
+                out["windows"].append({"nonce": [1, 2, 3, 4], "ntz": n, "worker_byte": wb,
+                                       "worker_bits": wbits, "k_begin": k0, "k_end": k0 + 4096,
+                                       "secret": secret, "global_idx": g, "local_idx": loc})
+
+    # 4) nonce lengths 0..80 (single block, two final blocks, midstate blocks)
+    for ln in list(range(0, 72)) + [100, 119, 120, 127, 128, 200]:
+        nonce = [(i * 37 + ln) & 0xFF for i in range(ln)]
+        for n in (2, 3):
+            secret, g, loc = py_mine(nonce, n)
+            out["nonce_lengths"].append({"nonce": nonce, "ntz": n, "secret": secret, "global_idx": g})
+
+    # 5) big cases via the C oracle (cross-checked on small cases first)
+    if args.big:
+        lib = load_oracle()
+        for e in out["first_hits"][:6]:
+            r = c_mine_parallel(lib, e["nonce"], e["ntz"], 1 << 20)
+            assert r is not None and r[0] == e["secret"] and r[1] == e["global_idx"], (e, r)
+        for nonce, n in (((1, 2, 3, 4), 7), ((2, 2, 2, 2), 7), ((2, 2, 2, 2), 8), ((1, 2, 3, 4), 8)):
+            secret, g, loc = c_mine_parallel(lib, nonce, n, 1 << 32)
+            exp = SURVEY_APPENDIX_A[(nonce, n)]
+            assert (secret, g) == (exp[0], exp[1]), (nonce, n, secret, g, exp)
+            assert has_num_zeroes_suffix(md5hex(nonce, secret), n)
+            out["first_hits"].append({"nonce": list(nonce), "ntz": n, "secret": secret, "global_idx": g,
+                                      "md5": md5hex(nonce, secret), "source": "c-oracle"})
+            print("big first hit", nonce, n, secret, g, file=sys.stderr)
+
+    with open(os.path.join(HERE, "pow_golden.json"), "w") as f:
+        json.dump(out, f, indent=0, separators=(",", ":"))
+        f.write("\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,68 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares (no GPU needed)."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for m in re.finditer(r"\b(dpow_[a-z0-9_]+)\s*\(", src):
+            names.add(m.group(1))
+    return names
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("dpow_open", "dpow_close", "dpow_cancel_flag", "dpow_search", "dpow_verify",
+                 "dpow_secret_from_index", "dpow_plan_window"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    import distpow
+    lib = distpow.lib()
+    missing = [n for n in sorted(declared_functions()) if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.check_output(["nm", "-D", "--defined-only", distpow.LIB_PATH]).decode()
+    exported = set(re.findall(r"\s[TW]\s+(dpow_[a-z0-9_]+)$", out, flags=re.M))
+    assert declared_functions() <= exported
+
+
+def test_library_is_gfx950_code_object():
+    import distpow
+    data = open(distpow.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"gfx942" not in data and b"gfx90a" not in data  # gfx950 only, no dual paths
+
+
+def test_abi_version_and_device_count():
+    import distpow
+    assert distpow.lib().dpow_abi_version() == 1
+    assert distpow.device_count() >= 0
+
+
+def test_open_without_gpu_fails_loudly():
+    import distpow
+    if distpow.device_count() > 0:
+        pytest.skip("a GPU is visible here")
+    with pytest.raises(distpow.DpowError):
+        distpow.Miner(0)
+
+
+def test_null_arguments_are_errors_not_crashes():
+    import distpow
+    L = distpow.lib()
+    assert L.dpow_search(None, b"", 0, 1, 0, 0, 0, 1, None, None, None) == -1
+    assert L.dpow_open(0, None) == -1
+    assert L.dpow_get_stats(None, None) == -1
+    L.dpow_close(None)  # no-op

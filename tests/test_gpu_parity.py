@@ -1,0 +1,170 @@
+"""GPU parity: the gfx950 search (through the C ABI) vs the oracle and the golden vectors.
+
+Bit-exact: secrets, global indices and "no hit" outcomes must equal the
+reference enumeration's (worker.go:301-400) for the same nonce, trailing-zero
+count and worker partition.  Run on the GPU box:  pytest -m gpu
+"""
+import hashlib
+import random
+import threading
+import time
+
+import pytest
+
+import distpow
+from distpow import CANCELLED, DPOW_NO_HIT, EXHAUSTED, FOUND
+
+pytestmark = pytest.mark.gpu
+
+
+def _hexz(nonce, secret):
+    return hashlib.md5(bytes(nonce) + bytes(secret)).hexdigest()
+
+
+def test_first_hits_golden(miner, golden):
+    """Configs 1, 2, 4 of BASELINE.json and SURVEY Appendix A (N = 0..8, workerBits = 0)."""
+    for e in golden["first_hits"]:
+        r = miner.mine(e["nonce"], e["ntz"])
+        assert r.status == FOUND, e
+        assert r.global_idx == e["global_idx"] and list(r.secret) == e["secret"], (e, r)
+        assert _hexz(e["nonce"], r.secret) == e["md5"]
+
+
+def test_partitions_golden(miner, golden):
+    for e in golden["partitions"]:
+        r = miner.mine(e["nonce"], e["ntz"], e["worker_byte"], e["worker_bits"])
+        assert r.status == FOUND and r.global_idx == e["global_idx"] and list(r.secret) == e["secret"], (e, r)
+
+
+def test_windows_golden(miner, golden):
+    for e in golden["windows"]:
+        r = miner.search(e["nonce"], e["ntz"], e["worker_byte"], e["worker_bits"], e["k_begin"], e["k_end"])
+        assert r.status == FOUND and r.global_idx == e["global_idx"] and list(r.secret) == e["secret"], (e, r)
+
+
+def test_nonce_lengths_golden(miner, golden):
+    """Every final-block layout (NBLK 1/2, W0, SH) and midstate nonces up to 200 bytes."""
+    for e in golden["nonce_lengths"]:
+        r = miner.mine(e["nonce"], e["ntz"])
+        assert r.status == FOUND and r.global_idx == e["global_idx"] and list(r.secret) == e["secret"], \
+            (len(e["nonce"]), e["ntz"], r)
+
+
+def test_random_windows_vs_oracle(miner, oracle):
+    """Random nonces, partitions and windows (hits and misses), oracle-sized."""
+    rnd = random.Random(416)
+    for it in range(150):
+        nlen = rnd.choice([0, 1, 2, 3, 4, 4, 4, 5, 7, 8, 16, 31, 50, 53, 54, 55, 56, 60, 61, 62, 63, 64, 65, 70, 127])
+        nonce = [rnd.randrange(256) for _ in range(nlen)]
+        wbits = rnd.choice([0, 0, 1, 2, 3, 4, 6, 8, 9, 10])
+        wb = rnd.randrange(1 << (wbits % 9)) if wbits % 9 else rnd.randrange(256)
+        rb = 8 - wbits % 9
+        ntz = rnd.choice([1, 2, 3, 3, 4, 4, 5])
+        seg = rnd.choice([0, 1, 2, 3, 4, 5])
+        k0 = rnd.randrange(1 << (8 * seg)) if seg else 0
+        if seg >= 3 and rnd.random() < 0.3:  # straddle a segment / 2^24 boundary
+            k0 = max(0, (1 << (8 * seg)) - rnd.randrange(1, 40))
+        nk = max(1, rnd.randrange(1, 1 + (1 << 16) // (1 << rb)))
+        k1 = min(k0 + nk, 1 << 40)
+        exp = oracle.mine_window(nonce, ntz, wb, wbits, k0, k1)
+        r = miner.search(nonce, ntz, wb, wbits, k0, k1)
+        if exp is None:
+            assert r.status == EXHAUSTED, (it, nonce, ntz, wb, wbits, k0, k1, r)
+        else:
+            assert r.status == FOUND and r.global_idx == exp[1] and list(r.secret) == exp[0], \
+                (it, nonce, ntz, wb, wbits, k0, k1, r, exp)
+
+
+def test_top_of_k_range(miner, oracle):
+    k0 = (1 << 40) - 2048
+    for ntz in (1, 2, 3):
+        exp = oracle.mine_window([9, 8, 7, 6], ntz, 0, 0, k0, 1 << 40)
+        r = miner.search([9, 8, 7, 6], ntz, 0, 0, k0, 1 << 40)
+        assert r.status == FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1])
+    with pytest.raises(distpow.DpowError):
+        miner.search([1], 1, 0, 0, 0, (1 << 40) + 1)
+
+
+def test_empty_window_and_unreachable(miner):
+    assert miner.search([1, 2, 3, 4], 3, 0, 0, 10, 10).status == EXHAUSTED
+    assert miner.search([1, 2, 3, 4], 33, 0, 0, 0, 1 << 16).status == EXHAUSTED  # N > 32 never matches
+    assert miner.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 20)).status == EXHAUSTED
+
+
+def test_ntz_zero_is_first_candidate(miner):
+    for wb, wbits in [(0, 0), (3, 2), (7, 3)]:
+        r = miner.mine([5, 6, 7, 8], 0, wb, wbits)
+        tb = distpow.thread_bytes(wb, wbits)[0]
+        assert r.status == FOUND and r.global_idx == tb and list(r.secret) == [tb]
+
+
+def test_bound_excludes_later_hits(miner, golden):
+    e = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 6)
+    g = e["global_idx"]
+    k1 = (g >> 8) + 10
+    assert miner.search(e["nonce"], 6, 0, 0, 0, k1, bound=g).status == EXHAUSTED
+    r = miner.search(e["nonce"], 6, 0, 0, 0, k1, bound=g + 1)
+    assert r.status == FOUND and r.global_idx == g
+
+
+def test_deterministic_repeats(miner):
+    rs = {miner.mine([1, 2, 3, 4], 7).global_idx for _ in range(3)}
+    assert rs == {231910082}
+
+
+def test_min_over_partitions_equals_wbits0_on_gpu(miner):
+    """Size-independent property at N = 9 (6.9e10 expected candidates, beyond the oracle):
+    the hit verifies by hashlib, and min over the 8 partitions (workerBits = 3) equals
+    the workerBits = 0 answer (the multi-GPU min-reduce rule)."""
+    nonce = [1, 2, 3, 4]
+    r0 = miner.mine(nonce, 9)
+    assert r0.status == FOUND
+    assert _hexz(nonce, r0.secret).endswith("0" * 9)
+    k_stop = (r0.global_idx >> 8) + 1
+    parts = [miner.search(nonce, 9, wb, 3, 0, k_stop) for wb in range(8)]
+    found = [p.global_idx for p in parts if p.status == FOUND]
+    assert min(found) == r0.global_idx
+    for p in parts:
+        if p.status == FOUND:
+            assert _hexz(nonce, p.secret).endswith("0" * 9)
+
+
+def test_cancel_flag_before_search(miner):
+    miner.cancel()
+    try:
+        assert miner.search([1, 2, 3, 4], 32, 0, 0, 0, 1 << 30).status == CANCELLED
+    finally:
+        miner.clear_cancel()
+    assert miner.search([1, 2, 3, 4], 3, 0, 0, 0, 1 << 10).status == FOUND
+
+
+def test_cancel_mid_search_latency(miner):
+    """Found/Cancel (worker.go:194,209) raise the pinned flag: the running kernel stops mid-launch."""
+    out = {}
+
+    def run():
+        t0 = time.perf_counter()
+        out["r"] = miner.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, 1 << 32)  # ~1.1e12 candidates: many seconds
+        out["t_end"] = time.perf_counter()
+        out["t0"] = t0
+
+    th = threading.Thread(target=run)
+    th.start()
+    time.sleep(0.3)
+    t_cancel = time.perf_counter()
+    miner.cancel()
+    th.join(timeout=30)
+    miner.clear_cancel()
+    assert not th.is_alive()
+    assert out["r"].status == CANCELLED
+    latency = out["t_end"] - t_cancel
+    print(f"cancel latency {latency * 1e3:.2f} ms")
+    assert latency < 0.25
+
+
+def test_stats_count_candidates(miner):
+    miner.reset_stats()
+    r = miner.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + 4096)
+    assert r.status == EXHAUSTED
+    s = miner.stats()
+    assert s.candidates == 4096 * 256 and s.launches == 1 and s.kernel_ms > 0

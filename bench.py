@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the VALU issue-rate probe")
+    ap.add_argument("--no-tts", action="store_true", help="skip the time-to-secret configs")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -119,7 +121,7 @@ def main():
     tts = {}
     ttsk = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8),
             ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5)]
-    for nonce, n in ttsk:
+    for nonce, n in ([] if args.no_tts else ttsk):
         barrier()
         t1 = time.perf_counter()
         res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
@@ -129,6 +131,13 @@ def main():
         assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
         tts[f"{bytes(nonce).hex()}/{n}"] = {"ms": round(dt * 1e3, 3), "global_idx": res.global_idx,
                                             "secret": list(res.secret)}
+
+    probe = {}
+    if rank == 0 and not args.no_probe:
+        from distpow._lib import VALU_KINDS, valu_rate
+        for kind, name in VALU_KINDS.items():
+            r, clk = valu_rate(local_rank, kind)
+            probe[name] = {"tops": round(r / 1e12, 3), "clock_ghz": round(clk, 3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -170,6 +179,7 @@ def main():
                 "launches": int(st.launches),
             },
             "stream_event_ms": round(stream_ms, 3),
+            "valu_probe": probe,
             "time_to_secret": tts,
             "cpu_baseline": cpu,
             "geometry": {"cus": cus, "threads_per_block": tpb},

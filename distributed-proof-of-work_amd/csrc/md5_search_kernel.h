@@ -28,6 +28,16 @@ namespace dpow {
 
 #define DPOW_DEV __device__ __forceinline__
 
+// SGPR budget: <= 80 allocated SGPRs admit 8 four-wave workgroups per CU
+// (8 waves per SIMD, MI355X_MICROARCH.md "Residency").  Literal K constants are
+// rematerialised by SALU moves, which co-issue beside other waves' VALU.
+#ifndef DPOW_ADD_MODE
+#define DPOW_ADD_MODE 0  // 0: compiler's choice (v_add3_u32); 1: two VOP2 v_add_u32
+#endif
+#ifndef DPOW_NUM_SGPR
+#define DPOW_NUM_SGPR 72
+#endif
+
 template <int I>
 DPOW_DEV uint32_t md5_fn(uint32_t x, uint32_t y, uint32_t z) {
     constexpr int r = I / 16;
@@ -48,14 +58,35 @@ DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &
         constexpr int ai = (64 - I) % 4, bi = (ai + 1) % 4, ci = (ai + 2) % 4, di = (ai + 3) % 4;
         constexpr int m = 16 * BLK + md5_word(I);
         constexpr int s = md5_shift(I);
-        const uint32_t kt = L.KT[64 * BLK + I];
+        // Words past the variable bytes, the chunk tail and the 0x80 pad -- every
+        // word after W0 + 2 except the bit-length word -- are zero for every launch
+        // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
+        constexpr bool zero_word = m > W0 + 2 && m != 16 * NBLK - 2;
+        const uint32_t kt = zero_word ? kMd5K[I] : L.KT[64 * BLK + I];
 #pragma unroll
         for (int j = 0; j < NCAND; ++j) {
             uint32_t km = kt;
             if constexpr (m == W0) km = (km + v.lo_s[j]) + v.lo_v;
             if constexpr (SH != 0 && m == W0 + 1) km += v.hi[j];
             const uint32_t f = md5_fn<I>(x[bi][j], x[ci][j], x[di][j]);
+#if DPOW_ADD_MODE == 1
+            // a + f + km as two full-rate VOP2 adds (K as an inline literal when the word is zero)
+            if constexpr (BLK > 0 || I > W0 + 1) {
+                uint32_t t;
+                if constexpr (zero_word)
+                    asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "i"(kMd5K[I]), "v"(x[ai][j]));
+                else if constexpr (m == W0 || (SH != 0 && m == W0 + 1))
+                    asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "v"(km), "v"(x[ai][j]));
+                else
+                    asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "s"(km), "v"(x[ai][j]));
+                asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "v"(f), "v"(t));
+                x[ai][j] = x[bi][j] + __builtin_rotateleft32(t, s);
+            } else {
+                x[ai][j] = x[bi][j] + __builtin_rotateleft32(x[ai][j] + f + km, s);
+            }
+#else
             x[ai][j] = x[bi][j] + __builtin_rotateleft32(x[ai][j] + f + km, s);
+#endif
         }
         md5_steps<NBLK, W0, SH, BLK, I + 1, NCAND>(x, L, v);
     }
@@ -129,7 +160,8 @@ DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
 }
 
 template <int NBLK, int W0, int SH>
-__global__ void __launch_bounds__(kBlockThreads) md5_search_kernel(const Launch L) {
+__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR)))
+md5_search_kernel(const Launch L) {
     constexpr uint32_t wpb = kBlockThreads / 64;
     if (blockIdx.x == 0) {  // dispatched first: the watcher
         watcher(L);

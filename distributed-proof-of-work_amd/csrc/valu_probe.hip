@@ -1,0 +1,157 @@
+// valu_probe.hip -- diagnostic: sustained VALU issue rate of the instructions the
+// MD5 search is made of (v_add_u32, v_add3_u32, v_alignbit_b32, v_bitop3_b32),
+// plus v_fma_f32 for reference, and the shader clock under that load.  It pins
+// the roofline "peak" that bench.py divides by: 8 independent dependency chains
+// per lane, 8 waves per SIMD, every CU busy.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/dpow_diag.h"
+
+namespace {
+
+constexpr int kChains = 8;
+constexpr int kUnroll = 16;
+constexpr int kThreads = 256;
+
+template <int KIND>
+__device__ __forceinline__ void op(uint32_t &a, uint32_t b, uint32_t c) {
+    if constexpr (KIND == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (KIND == 1) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 2) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a) : "v"(b));
+    if constexpr (KIND == 3) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 4) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 6) asm volatile("v_lshl_add_u32 %0, %0, 7, %1" : "+v"(a) : "v"(b));
+    if constexpr (KIND == 7) asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(a) : "v"(b));
+    if constexpr (KIND == 8) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 9) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 10) asm volatile("v_lshlrev_b32 %0, 7, %0" : "+v"(a));
+    if constexpr (KIND == 11) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 12) asm volatile("v_add_u32 %0, 0x5a827999, %0" : "+v"(a));
+    if constexpr (KIND == 13) asm volatile("v_alignbyte_b32 %0, %0, %0, 2" : "+v"(a));
+    if constexpr (KIND == 14) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 15) asm volatile("v_add_lshl_u32 %0, %0, %1, 7" : "+v"(a) : "v"(b));
+    if constexpr (KIND == 16) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (KIND == 17) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "s"(b), "v"(c));
+    if constexpr (KIND == 18) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a) : "v"(b));
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(kThreads) valu_probe_kernel(uint32_t *out, uint32_t iters, uint64_t *clk) {
+    uint32_t x[kChains];
+    const uint32_t b = KIND == 17 ? __builtin_amdgcn_readfirstlane(blockIdx.x * 0x9E3779B9u)
+                                  : threadIdx.x * 0x9E3779B9u;
+    const uint32_t c = blockIdx.x + 0x7F4A7C15u + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kChains; ++j) x[j] = threadIdx.x + 17u * j;
+    uint64_t t0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+#pragma unroll
+            for (int j = 0; j < kChains; ++j) {
+                if constexpr (KIND == 5) {
+                    uint32_t f = x[j];
+                    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(f) : "v"(x[j]), "v"(b), "v"(c));
+                    asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[j]) : "v"(f), "v"(c));
+                    asm volatile("v_alignbit_b32 %0, %0, %0, 25" : "+v"(x[j]));
+                    asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j]) : "v"(b));
+                } else {
+                    op<KIND>(x[j], b, c);
+                }
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < kChains; ++j) acc ^= x[j];
+    out[blockIdx.x * kThreads + threadIdx.x] = acc;
+}
+
+template <int KIND>
+hipError_t run(uint32_t blocks, uint32_t iters, uint32_t *out, uint64_t *clk, hipStream_t s) {
+    hipLaunchKernelGGL(valu_probe_kernel<KIND>, dim3(blocks), dim3(kThreads), 0, s, out, iters, clk);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz) {
+    if (kind < 0 || kind > 18 || !lane_ops_per_s || !clock_ghz) return -1;
+    if (hipSetDevice(device) != hipSuccess) return -2;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -2;
+    const uint32_t blocks = (uint32_t)prop.multiProcessorCount * 8;  // 32 waves per CU = 8 per SIMD
+    const uint32_t iters = 4096;
+    uint32_t *out = nullptr;
+    uint64_t *clk = nullptr;
+    if (hipMalloc(&out, (size_t)blocks * kThreads * 4) != hipSuccess) return -2;
+    if (hipMalloc(&clk, (size_t)blocks * 16) != hipSuccess) return -2;
+    hipStream_t s;
+    hipEvent_t e0, e1;
+    (void)hipStreamCreate(&s);
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    auto launch = [&]() -> hipError_t {
+        switch (kind) {
+            case 0: return run<0>(blocks, iters, out, clk, s);
+            case 1: return run<1>(blocks, iters, out, clk, s);
+            case 2: return run<2>(blocks, iters, out, clk, s);
+            case 3: return run<3>(blocks, iters, out, clk, s);
+            case 4: return run<4>(blocks, iters, out, clk, s);
+            case 5: return run<5>(blocks, iters, out, clk, s);
+            case 6: return run<6>(blocks, iters, out, clk, s);
+            case 7: return run<7>(blocks, iters, out, clk, s);
+            case 8: return run<8>(blocks, iters, out, clk, s);
+            case 9: return run<9>(blocks, iters, out, clk, s);
+            case 10: return run<10>(blocks, iters, out, clk, s);
+            case 11: return run<11>(blocks, iters, out, clk, s);
+            case 12: return run<12>(blocks, iters, out, clk, s);
+            case 13: return run<13>(blocks, iters, out, clk, s);
+            case 14: return run<14>(blocks, iters, out, clk, s);
+            case 15: return run<15>(blocks, iters, out, clk, s);
+            case 16: return run<16>(blocks, iters, out, clk, s);
+            case 17: return run<17>(blocks, iters, out, clk, s);
+            default: return run<18>(blocks, iters, out, clk, s);
+        }
+    };
+    hipError_t err = hipSuccess;
+    for (int w = 0; w < 3 && err == hipSuccess; ++w) err = launch();  // warm the clock
+    (void)hipEventRecord(e0, s);
+    const int reps = 5;
+    for (int r = 0; r < reps && err == hipSuccess; ++r) err = launch();
+    (void)hipEventRecord(e1, s);
+    (void)hipStreamSynchronize(s);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::vector<uint64_t> h(2 * blocks);
+    (void)hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost);
+    double ratio = 0;
+    uint32_t n = 0;
+    for (uint32_t bI = 0; bI < blocks; ++bI)
+        if (h[2 * bI + 1]) {
+            ratio += (double)h[2 * bI] / (double)h[2 * bI + 1];
+            ++n;
+        }
+    const double instr_per_lane = (double)iters * kUnroll * kChains * (kind == 5 ? 4 : 1);
+    *lane_ops_per_s = instr_per_lane * (double)blocks * kThreads * reps / (ms * 1e-3);
+    *clock_ghz = n ? ratio / n * 0.1 : 0.0;  // s_memrealtime ticks at 100 MHz
+    (void)hipFree(out);
+    (void)hipFree(clk);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(s);
+    return err == hipSuccess ? 0 : -2;
+}

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdpow.so")
+# DPOW_LIB_PATH overrides the in-tree library (A/B builds in tools/ab_variants.py only).
+LIB_PATH = os.environ.get("DPOW_LIB_PATH") or os.path.join(_HERE, "libdpow.so")
 
 DPOW_NO_HIT = 0x7FFFFFFFFFFFFFFF
 DPOW_MAX_SECRET = 16
@@ -86,6 +87,8 @@ def lib():
         "dpow_last_error": (ctypes.c_char_p, []),
         "dpow_abi_version": (ctypes.c_int, []),
         "dpow_device_count": (ctypes.c_int, []),
+        "dpow_diag_valu_rate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -93,6 +96,21 @@ def lib():
         fn.argtypes = args
     _lib = L
     return L
+
+
+VALU_KINDS = {0: "v_add_u32", 1: "v_add3_u32", 2: "v_alignbit_b32", 3: "v_bitop3_b32", 4: "v_fma_f32",
+              5: "md5_step_mix", 6: "v_lshl_add_u32", 7: "v_lshl_or_b32", 8: "v_xad_u32", 9: "v_perm_b32",
+              10: "v_lshlrev_b32", 11: "v_or3_b32", 12: "v_add_u32_literal", 13: "v_alignbyte_b32",
+              14: "v_bfi_b32", 15: "v_add_lshl_u32", 16: "v_xor_b32", 17: "v_add3_u32_sgpr", 18: "v_pk_add_u16"}
+
+
+def valu_rate(device=0, kind=5):
+    """(lane-ops/s, in-kernel clock GHz) of one VALU instruction kind with every CU busy."""
+    r, c = ctypes.c_double(), ctypes.c_double()
+    code = lib().dpow_diag_valu_rate(device, kind, ctypes.byref(r), ctypes.byref(c))
+    if code < 0:
+        raise DpowError(code, "dpow_diag_valu_rate failed")
+    return r.value, c.value
 
 
 def last_error():

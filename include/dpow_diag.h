@@ -1,0 +1,26 @@
+/*
+ * dpow_diag.h -- diagnostics of libdpow.so (not part of the reference's
+ * interface): measures what bounds the search kernel on this device.
+ */
+#ifndef DPOW_DIAG_H
+#define DPOW_DIAG_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Sustained VALU issue rate on `device` for one instruction kind, all CUs busy
+ * (8 waves per SIMD, 8 independent chains per lane):
+ *   kind 0 v_add_u32, 1 v_add3_u32, 2 v_alignbit_b32, 3 v_bitop3_b32,
+ *        4 v_fma_f32, 5 the MD5 step mix (bitop3, add3, alignbit, add),
+ *        6 v_lshl_add_u32, 7 v_lshl_or_b32, 8 v_xad_u32, 9 v_perm_b32, 10 v_lshlrev_b32,
+ *        11 v_or3_b32, 12 v_add_u32 with a literal, 13 v_alignbyte_b32, 14 v_bfi_b32,
+ *        15 v_add_lshl_u32, 16 v_xor_b32, 17 v_add3_u32 with an SGPR operand, 18 v_pk_add_u16.
+ * *lane_ops_per_s = wave64 instructions x 64 / s; *clock_ghz = mean in-kernel
+ * shader clock (s_memtime / s_memrealtime).  Returns 0, or < 0 on error. */
+int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPOW_DIAG_H */

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""A/B throughput of libdpow builds: tools/ab_variants.py lib1.so lib2.so ...
+
+Each library runs in its own process (fresh HIP runtime), interleaved over
+several rounds; prints GH/s of the bench sweep (nonce [1,2,3,4], N=32,
+2^34 candidates per trial in the L=4 segment) per library and round.
+"""
+import json
+import os
+import subprocess
+import sys
+
+CHILD = r"""
+import os, sys, time, json
+sys.path.insert(0, os.path.join(os.environ["ROOT"], "distributed-proof-of-work_amd"))
+import torch, distpow
+m = distpow.Miner(0)
+K0 = 1 << 24
+n = (1 << 34) >> 8
+m.search([1,2,3,4], 32, 0, 0, K0, K0 + n)   # warm
+res = []
+for t in range(3):
+    m.reset_stats()
+    t0 = time.perf_counter()
+    m.search([1,2,3,4], 32, 0, 0, K0 + (t+1)*n, K0 + (t+2)*n)
+    dt = time.perf_counter() - t0
+    st = m.stats()
+    res.append({"wall_ghs": (1 << 34) / dt / 1e9, "kernel_ghs": st.candidates / (st.kernel_ms * 1e-3) / 1e9})
+print(json.dumps(res))
+"""
+
+def main():
+    libs = sys.argv[1:]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {l: [] for l in libs}
+    for rnd in range(2):
+        for l in libs:
+            env = dict(os.environ, DPOW_LIB_PATH=os.path.abspath(l), ROOT=root)
+            r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                print(l, "FAILED", r.stderr[-2000:], flush=True)
+                continue
+            res = json.loads(r.stdout.strip().splitlines()[-1])
+            out[l] += res
+            print(rnd, l, " ".join(f"{x['kernel_ghs']:.1f}" for x in res), flush=True)
+    for l, rs in out.items():
+        if rs:
+            ks = sorted(x["kernel_ghs"] for x in rs)
+            print(f"{l}: median kernel {ks[len(ks)//2]:.2f} GH/s  max {ks[-1]:.2f}", flush=True)
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,17 @@ class PlanLaunch(ctypes.Structure):
                 ("chunk_len", ctypes.c_uint32)]
 
 
+DPOW_MAX_NONCE = 1024
+EPROTO, ETIMEOUT = -6, -7
+
+
+class WorkerResult(ctypes.Structure):
+    _fields_ = [("num_trailing_zeros", ctypes.c_uint32), ("worker_byte", ctypes.c_uint32),
+                ("has_secret", ctypes.c_uint32), ("secret_len", ctypes.c_uint32),
+                ("secret", ctypes.c_uint8 * DPOW_MAX_SECRET), ("token", ctypes.c_uint64),
+                ("nonce_len", ctypes.c_uint64), ("nonce", ctypes.c_uint8 * DPOW_MAX_NONCE)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("searches", ctypes.c_uint64), ("launches", ctypes.c_uint64),
                 ("candidates", ctypes.c_uint64), ("kernel_ms", ctypes.c_double)]
@@ -89,6 +100,17 @@ def lib():
         "dpow_device_count": (ctypes.c_int, []),
         "dpow_diag_valu_rate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(ctypes.c_double)]),
+        "dpow_worker_new": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+        "dpow_worker_free": (None, [vp]),
+        "dpow_worker_mine": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint64]),
+        "dpow_worker_found": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64]),
+        "dpow_worker_cancel": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
+                                              ctypes.c_uint32]),
+        "dpow_worker_next_result": (ctypes.c_int, [vp, ctypes.POINTER(WorkerResult), ctypes.c_int]),
+        "dpow_worker_trace": (ctypes.c_size_t, [vp, ctypes.c_char_p, ctypes.c_size_t]),
+        "dpow_worker_active_tasks": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,80 @@
+"""Python handle on the native GPU worker (include/dpow_worker.h).
+
+Mirrors the reference worker's RPC surface (worker.go:108-232): Mine, Found,
+Cancel, and the ResultChannel drained by cmd/worker/main.go:27-36.  The miner
+(worker.go:258-401), its cache (worker.go:424-506) and its trace actions run
+natively in libdpow.so; the search loop runs on the GPU.
+"""
+import ctypes
+import json
+from dataclasses import dataclass
+from typing import List, Optional
+
+from ._lib import ETIMEOUT, DpowError, WorkerResult, check, lib
+
+
+@dataclass
+class WorkerResultWithToken:
+    """worker.go:38-44; secret None is the nil-secret cancellation ACK."""
+    nonce: bytes
+    num_trailing_zeros: int
+    worker_byte: int
+    secret: Optional[bytes]
+    token: int
+
+
+class Worker:
+    def __init__(self, device: int = 0):
+        self._w = ctypes.c_void_p()
+        check(lib().dpow_worker_new(device, ctypes.byref(self._w)), "dpow_worker_new")
+        self.device = device
+
+    def close(self):
+        if self._w:
+            lib().dpow_worker_free(self._w)
+            self._w = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- RPCs ------------------------------------------------------------------
+    def mine(self, nonce, num_trailing_zeros, worker_byte, worker_bits, token=0):
+        n = bytes(nonce)
+        check(lib().dpow_worker_mine(self._w, n, len(n), num_trailing_zeros, worker_byte, worker_bits, token),
+              "WorkerRPCHandler.Mine")
+
+    def found(self, nonce, num_trailing_zeros, worker_byte, secret, token=0):
+        n, s = bytes(nonce), bytes(secret)
+        check(lib().dpow_worker_found(self._w, n, len(n), num_trailing_zeros, worker_byte, s, len(s), token),
+              "WorkerRPCHandler.Found")
+
+    def cancel(self, nonce, num_trailing_zeros, worker_byte):
+        n = bytes(nonce)
+        return check(lib().dpow_worker_cancel(self._w, n, len(n), num_trailing_zeros, worker_byte),
+                     "WorkerRPCHandler.Cancel")
+
+    # -- ResultChannel -----------------------------------------------------------
+    def next_result(self, timeout_ms: int = -1) -> Optional[WorkerResultWithToken]:
+        r = WorkerResult()
+        code = lib().dpow_worker_next_result(self._w, ctypes.byref(r), timeout_ms)
+        if code == ETIMEOUT:
+            return None
+        check(code, "dpow_worker_next_result")
+        return WorkerResultWithToken(bytes(r.nonce[:r.nonce_len]), r.num_trailing_zeros, r.worker_byte,
+                                     bytes(r.secret[:r.secret_len]) if r.has_secret else None, r.token)
+
+    # -- introspection -------------------------------------------------------------
+    def trace(self) -> List[dict]:
+        n = lib().dpow_worker_trace(self._w, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().dpow_worker_trace(self._w, buf, n + 1)
+        return [json.loads(l) for l in buf.value.decode().splitlines() if l]
+
+    def active_tasks(self) -> int:
+        return lib().dpow_worker_active_tasks(self._w)
+
+
+__all__ = ["Worker", "WorkerResultWithToken", "DpowError"]

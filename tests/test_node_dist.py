@@ -1,0 +1,80 @@
+"""N>1 path of the node scheduler (distpow.node.node_mine) on CPU with gloo.
+
+Each rank owns the prefix partition (worker_byte = rank, worker_bits = log2 W,
+coordinator.go:127,326); all ranks scan the same k-window per batch and an
+all-reduce MIN of [best index, running] ends the search.  The per-rank search
+here is the oracle (test injection: the product passes Miner.search), so the
+collective logic is checked against the golden workerBits = 0 answers.
+"""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_search_fn():
+    from _oracle import Oracle
+    from distpow import search as S
+    o = Oracle()
+
+    def fn(nonce, ntz, wb, wbits, k0, k1, bound):
+        r = o.mine_window(list(nonce), ntz, wb, wbits, k0, k1)
+        if r is None or r[1] >= bound:
+            return S.SearchResult(S.EXHAUSTED)
+        return S.SearchResult(S.FOUND, r[1], bytes(r[0]))
+    return fn
+
+
+def _worker(rank, world, port, cases, out_q, cancel_rank):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+    import torch.distributed as dist
+    from distpow.node import node_mine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    fn = _oracle_search_fn()
+    res = []
+    for nonce, ntz in cases:
+        r = node_mine(fn, nonce, ntz, rank, world, batch_k=64)
+        res.append((r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner, r.batches))
+    # cancellation vote: one rank reports cancelled -> every rank stops at the same batch
+    r = node_mine(fn, [1, 2, 3, 4], 32, rank, world, batch_k=16, k_limit=1 << 20,
+                  cancelled=(lambda: rank == cancel_rank))
+    res.append((r.status, r.batches))
+    out_q.put((rank, res))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_node_mine_gloo_matches_wbits0_answer(golden, world):
+    cases = [(e["nonce"], e["ntz"]) for e in golden["first_hits"] if e["global_idx"] < 200_000]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, world - 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = {(tuple(e["nonce"]), e["ntz"]): e for e in golden["first_hits"]}
+    for rank in range(world):
+        res = outs[rank]
+        for (nonce, ntz), (status, g, secret, owner, batches) in zip(cases, res[:-1]):
+            e = exp[(tuple(nonce), ntz)]
+            assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, nonce, ntz)
+            assert owner == (g & 0xFF) >> (8 - (world.bit_length() - 1))
+        assert res[-1] == (2, 1)  # CANCELLED after the first batch on every rank
+    # all ranks agree batch by batch
+    assert len({tuple(map(tuple, [r[:2] for r in outs[k][:-1]])) for k in outs}) == 1

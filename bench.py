@@ -37,6 +37,7 @@ NONCE = [1, 2, 3, 4]
 SWEEP_NTZ = 32
 CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 K0 = 1 << 24                      # start of the L = 4 segment
+TTS_BATCH_K = 1 << 22              # time-to-secret batches: 2^30 candidates per batch over all ranks
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
 # INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,
 # the MI355X_MICROARCH.md FP32 vector peak (157.3 TFLOP/s) / 2 FLOP per FMA lane-op.
@@ -57,6 +58,10 @@ def main():
     ap.add_argument("--no-tts", action="store_true", help="skip the time-to-secret configs")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (gloo + --same-device only to rehearse the N>1 path on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal: every rank searches on device 0 (with --backend gloo)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -64,15 +69,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
+    device = 0 if args.same_device else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
     wb, wbits = partition_of_rank(rank, world)
     R = 1 << (8 - wbits)
     batch_k = CANDIDATES_PER_GPU_PER_STEP // R  # same k-window on every rank
 
-    miner = distpow.Miner(local_rank)
-    dev = torch.device("cuda", local_rank)
+    miner = distpow.Miner(device)
+    dev = torch.device("cuda", device) if args.backend == "nccl" else torch.device("cpu")
     red = torch.empty(2, dtype=torch.int64, device=dev)
 
     def step(s):
@@ -104,7 +113,7 @@ def main():
     elapsed = time.perf_counter() - t0
     st = miner.stats()
     stream_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
@@ -125,7 +134,7 @@ def main():
         barrier()
         t1 = time.perf_counter()
         res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
-                        batch_k=(1 << 26) >> (8 - wbits) if wbits else 1 << 26, device=dev)
+                        batch_k=TTS_BATCH_K, device=dev)
         barrier()
         dt = time.perf_counter() - t1
         assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
@@ -136,7 +145,7 @@ def main():
     if rank == 0 and not args.no_probe:
         from distpow._lib import VALU_KINDS, valu_rate
         for kind, name in VALU_KINDS.items():
-            r, clk = valu_rate(local_rank, kind)
+            r, clk = valu_rate(device, kind)
             probe[name] = {"tops": round(r / 1e12, 3), "clock_ghz": round(clk, 3)}
 
     cpu = None

@@ -1,11 +1,12 @@
 // dpow_api.cpp -- the C ABI (include/dpow.h) over the gfx950 search kernels.
 //
 // dpow_search replaces the reference miner's enumeration loop
-// (worker.go:301-400): plan the window into launches (plan.cpp), queue them all
-// on the context's stream behind one control-block reset, read the control
-// block back once, and re-verify a hit with the host MD5 before returning it.
-// Launches queued after a hit (or a cancel) retire immediately: every worker
-// wave compares its first index against Ctrl::best / Ctrl::stop first.
+// (worker.go:301-400): plan the window into launches (plan.cpp), queue them on
+// the context's stream behind one control-block reset with at most kDepth in
+// flight (a pinned snapshot of the control block follows each launch), and
+// re-verify a hit with the host MD5 before returning it.  Launches queued after
+// a hit (or a cancel) retire at once: every worker wave compares its first
+// index against Ctrl::best / Ctrl::stop before hashing.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -40,11 +41,14 @@ int hip_fail(hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_fail(e_, #call); \
     } while (0)
 
-// Worker waves to aim for per launch: enough rounds of the device's resident
-// waves that the last round's imbalance is small.
-constexpr uint64_t kRoundsPerLaunch = 16;
-constexpr uint64_t kResidentWavesPerCu = 24;
-constexpr uint32_t kMaxIters = 1024;
+// Persistent grid: one round of resident workgroups (8 four-wave workgroups per
+// CU at <= 80 SGPRs), work handed out by in-order chunk claims.  A chunk is
+// sized for >= 16 claims per wave (small tail) and at most 32 wave-blocks
+// (one claim counter serves < 88 claims/us, MI355X_MICROARCH.md "dequeue").
+constexpr uint64_t kBlocksPerCu = 8;
+constexpr uint64_t kClaimsPerWave = 16;
+constexpr uint64_t kMaxChunk = 32;
+constexpr size_t kClaimRing = 1024;  // per-launch claim counters, zeroed per search
 // Launches kept in flight: launch j is queued only after the control block
 // snapshot behind launch j - kDepth shows no hit and no cancel, so a hit or a
 // cancel leaves at most kDepth launches to retire (each exits at its first check).
@@ -57,6 +61,7 @@ struct dpow_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     Ctrl *d_ctrl = nullptr;
+    unsigned long long *d_claims = nullptr;  // kClaimRing claim counters
     Ctrl *h_ctrl = nullptr;        // pinned staging: [0] reset image, [1 + j % kRing] snapshots
     uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped
     uint32_t *d_cancel = nullptr;  // device alias
@@ -99,6 +104,7 @@ int dpow_open(int device, dpow_ctx **out) {
     c->cus = (uint32_t)prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&c->d_ctrl, sizeof(Ctrl))) != hipSuccess ||
+        (e = hipMalloc(&c->d_claims, kClaimRing * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_ctrl, (1 + kRing) * sizeof(Ctrl), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_cancel, 64, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_cancel), c->h_cancel, 0)) != hipSuccess) {
@@ -116,6 +122,7 @@ void dpow_close(dpow_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
     if (c->d_ctrl) (void)hipFree(c->d_ctrl);
+    if (c->d_claims) (void)hipFree(c->d_claims);
     if (c->h_ctrl) (void)hipHostFree(c->h_ctrl);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -129,7 +136,7 @@ int dpow_device(dpow_ctx *c) { return c ? c->device : -1; }
 int dpow_geometry(dpow_ctx *c, uint32_t *cus, uint32_t *blocks_per_cu, uint32_t *threads_per_block) {
     if (!c) return set_error(DPOW_EINVAL, "dpow_geometry: ctx is NULL");
     if (cus) *cus = c->cus;
-    if (blocks_per_cu) *blocks_per_cu = (uint32_t)(kResidentWavesPerCu / (kBlockThreads / 64));
+    if (blocks_per_cu) *blocks_per_cu = (uint32_t)kBlocksPerCu;
     if (threads_per_block) *threads_per_block = kBlockThreads;
     return 0;
 }
@@ -219,31 +226,31 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         c->events.push_back(ev);
     }
 
-    const uint64_t target_waves = (uint64_t)c->cus * kResidentWavesPerCu * kRoundsPerLaunch;
     constexpr uint32_t wpb = kBlockThreads / 64;
+    const size_t nz = c->plan.size() < kClaimRing ? c->plan.size() : kClaimRing;
+    DPOW_HIP(hipMemsetAsync(c->d_claims, 0, nz * sizeof(unsigned long long), c->stream));
     uint32_t done_target = 0;
     uint64_t candidates = 0;
     size_t launched = 0;
-    bool stop_early = false;
     for (size_t li = 0; li < c->plan.size(); ++li) {
         if (li >= kDepth) {  // look at the snapshot behind launch li - kDepth
             DPOW_HIP(hipEventSynchronize(c->events[2 * (li - kDepth) + 1]));
             const Ctrl &snap = c->h_ctrl[1 + (li - kDepth) % kRing];
-            if (snap.best < bound || snap.stop != 0u || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) {
-                stop_early = true;
-                break;
-            }
+            if (snap.best < bound || snap.stop != 0u || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) break;
         }
         PlannedLaunch &pl = c->plan[li];
         Launch &L = pl.L;
-        uint64_t iters = L.n_wblocks / target_waves;
-        if (iters < 1) iters = 1;
-        if (iters > kMaxIters) iters = kMaxIters;
-        const uint64_t waves = (L.n_wblocks + iters - 1) / iters;
-        const uint64_t worker_blocks = (waves + wpb - 1) / wpb;
-        if (worker_blocks + 1 > 0x7FFFFFFFull) return set_error(DPOW_ERANGE, "dpow_search: grid too large");
+        unsigned long long *claim = c->d_claims + li % kClaimRing;
+        if (li >= kClaimRing) DPOW_HIP(hipMemsetAsync(claim, 0, sizeof(unsigned long long), c->stream));
+        uint64_t worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
+        if (worker_blocks > (uint64_t)c->cus * kBlocksPerCu) worker_blocks = (uint64_t)c->cus * kBlocksPerCu;
+        uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
+        if (chunk < 1) chunk = 1;
+        if (chunk > kMaxChunk) chunk = kMaxChunk;
         done_target += (uint32_t)(worker_blocks * wpb);
-        L.iters = (uint32_t)iters;
+        L.chunk = (uint32_t)chunk;
+        L.n_chunks = (L.n_wblocks + chunk - 1) / chunk;
+        L.claim = claim;
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;
         L.cancel = c->d_cancel;
@@ -257,7 +264,6 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         candidates += L.i_end - L.i_begin;
         ++launched;
     }
-    (void)stop_early;
     DPOW_HIP(hipStreamSynchronize(c->stream));
     const Ctrl fin = c->h_ctrl[1 + (launched - 1) % kRing];
 

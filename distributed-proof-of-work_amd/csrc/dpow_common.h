@@ -77,7 +77,9 @@ struct Launch {
     uint32_t dmask;        // mask on the final D word for min(ntz, 8) trailing nibbles
     uint32_t ntz;          // requested trailing zeros (full digest check when > 8)
     uint32_t done_target;  // watcher exits when Ctrl::done reaches this
-    uint32_t iters;        // wave-blocks per worker wave (contiguous run)
+    uint32_t chunk;        // wave-blocks per claim
+    uint64_t n_chunks;     // claims covering n_wblocks
+    unsigned long long *claim;  // this launch's claim counter (zeroed before the launch)
     Ctrl *ctrl;
     const uint32_t *cancel;  // device-visible alias of the pinned host cancel flag
 };

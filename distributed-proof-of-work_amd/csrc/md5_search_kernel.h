@@ -9,8 +9,9 @@
 //
 // Work decomposition: local index i = k * R + t (the reference's order, k outer,
 // t inner).  A wave-block is 64 * kNC consecutive indices (lane l, slot j ->
-// i0 + 64 j + l).  Worker waves walk wave-blocks grid-stride in increasing
-// order; the first hit of a wave-block (lowest slot, then lowest lane) goes to
+// i0 + 64 j + l).  Worker waves of a persistent grid claim chunks of
+// consecutive wave-blocks from an atomic counter, in increasing order; the
+// first hit of a wave-block (lowest slot, then lowest lane) goes to
 // atomicMin on the global index g = k * 256 + threadByte, which is monotone in
 // i, so the minimum is the reference's first hit.  A wave stops at the first
 // wave-block whose first index is >= the current minimum, so every candidate
@@ -150,6 +151,15 @@ DPOW_DEV void watcher(const Launch &L) {
     }
 }
 
+// One returning atomic per claim, by lane 0, broadcast to the wave.
+DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t lane) {
+    unsigned long long v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
     lo = lo < 0 ? 0 : (lo > 64 ? 64 : lo);
     hi = hi < 0 ? 0 : (hi > 64 ? 64 : hi);
@@ -159,70 +169,86 @@ DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
     return upto_hi & ~below_lo;
 }
 
+// Hash one wave-block (64 * kNC consecutive local indices from i0) and publish
+// its first hit, if any, to Ctrl::best.  Returns the wave's updated best.
+template <int NBLK, int W0, int SH>
+DPOW_DEV unsigned long long hash_wave_block(const Launch &L, uint64_t i0, uint32_t lane, uint32_t loff,
+                                            unsigned long long best) {
+    uint32_t vs[kNC];
+    VarWords v;
+#pragma unroll
+    for (int j = 0; j < kNC; ++j) {
+        vs[j] = wave_uniform_v(i0 + 64u * j, L.rbits, L.base_tb);
+        var_words<SH>(v, j, vs[j], loff);
+    }
+    uint32_t dig[4][kNC];
+    md5_tail<NBLK, W0, SH, kNC>(dig, L, v);
+
+    uint64_t bal[kNC];
+    uint64_t any = 0;
+#pragma unroll
+    for (int j = 0; j < kNC; ++j) {
+        bal[j] = __ballot((dig[3][j] & L.dmask) == 0u);
+        any |= bal[j];
+    }
+    if (any != 0) {  // rare (16^-N per candidate): lowest valid slot, then lowest lane
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+            const uint64_t ij = i0 + 64u * j;
+            uint64_t m = bal[j] & lane_range_mask((int64_t)(L.i_begin - ij), (int64_t)(L.i_end - ij));
+            if (m != 0 && L.ntz > 8u) {
+                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, vs[j], loff);
+                m = __ballot(ok);
+            }
+            if (m != 0) {
+                const uint64_t g = global_of_local(ij + (uint64_t)__builtin_ctzll(m), L.rbits, L.base_tb);
+                if (lane == 0) atomicMin(&L.ctrl->best, (unsigned long long)g);
+                return g < best ? g : best;
+            }
+        }
+    }
+    return best;
+}
+
 template <int NBLK, int W0, int SH>
 __global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR)))
 md5_search_kernel(const Launch L) {
-    constexpr uint32_t wpb = kBlockThreads / 64;
     if (blockIdx.x == 0) {  // dispatched first: the watcher
         watcher(L);
         return;
     }
     const uint32_t lane = threadIdx.x & 63u;
-    // Worker wave w owns the contiguous run of wave-blocks [w * iters, (w + 1) * iters).
-    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x - 1) * wpb + (threadIdx.x >> 6));
-    const uint64_t b_begin = (uint64_t)wave * L.iters;
-    const uint64_t b_end = b_begin + L.iters < L.n_wblocks ? b_begin + L.iters : L.n_wblocks;
     const uint32_t loff = lane_offset(L.rbits, lane);
 
     unsigned long long best = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t stop = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-    for (uint64_t b = b_begin; b < b_end; ++b) {
-        const uint64_t i0 = L.wb_begin + b * (uint64_t)kWaveBlock;
-        const uint64_t ifirst = i0 < L.i_begin ? L.i_begin : i0;
-        if (stop != 0u || global_of_local(ifirst, L.rbits, L.base_tb) >= best) break;
-        // Issued now, consumed at the next wave-block: the load latency hides
-        // behind this wave-block's ~kNC*250 VALU instructions.
+    // Waves claim chunks of L.chunk consecutive wave-blocks from one counter, so
+    // claims are handed out in increasing index order (the early exit stays
+    // exact) and neither the grid size nor the residency creates a tail.  The
+    // next claim is requested while the current chunk is hashed.
+    uint64_t claim = claim_next(L.claim, lane);
+    while (claim < L.n_chunks) {
+        const uint64_t next = claim_next(L.claim, lane);
+        const uint64_t b_begin = claim * L.chunk;
+        const uint32_t nb = (uint32_t)(b_begin + L.chunk < L.n_wblocks ? L.chunk : L.n_wblocks - b_begin);
+        const uint64_t i_first = L.wb_begin + b_begin * (uint64_t)kWaveBlock;
+        // Early exit at chunk granularity (<= 32 wave-blocks): stop on a cancel,
+        // or once this chunk starts at or above the best index found so far.
+        // Everything below the best has been or is being hashed by earlier claims.
+        if (stop != 0u ||
+            global_of_local(i_first < L.i_begin ? L.i_begin : i_first, L.rbits, L.base_tb) >= best)
+            break;
+        // Issued now, consumed at the next claim: the latency hides behind the chunk.
         const unsigned long long best_next =
             __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t stop_next = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-        uint32_t vs[kNC];
-        VarWords v;
-#pragma unroll
-        for (int j = 0; j < kNC; ++j) {
-            vs[j] = wave_uniform_v(i0 + 64u * j, L.rbits, L.base_tb);
-            var_words<SH>(v, j, vs[j], loff);
-        }
-        uint32_t dig[4][kNC];
-        md5_tail<NBLK, W0, SH, kNC>(dig, L, v);
-
-        uint64_t bal[kNC];
-        uint64_t any = 0;
-#pragma unroll
-        for (int j = 0; j < kNC; ++j) {
-            bal[j] = __ballot((dig[3][j] & L.dmask) == 0u);
-            any |= bal[j];
-        }
-        if (any != 0) {
-#pragma unroll
-            for (int j = 0; j < kNC; ++j) {
-                const uint64_t ij = i0 + 64u * j;
-                uint64_t m = bal[j] & lane_range_mask((int64_t)(L.i_begin - ij), (int64_t)(L.i_end - ij));
-                if (m != 0 && L.ntz > 8u) {
-                    const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, vs[j], loff);
-                    m = __ballot(ok);
-                }
-                if (m != 0) {
-                    const uint64_t g = global_of_local(ij + (uint64_t)__builtin_ctzll(m), L.rbits, L.base_tb);
-                    if (lane == 0) atomicMin(&L.ctrl->best, (unsigned long long)g);
-                    if (g < best) best = g;
-                    break;
-                }
-            }
-        }
+        uint64_t i0 = i_first;
+        for (uint32_t r = 0; r < nb; ++r, i0 += (uint64_t)kWaveBlock)
+            best = hash_wave_block<NBLK, W0, SH>(L, i0, lane, loff, best);
         best = best_next < best ? best_next : best;
         stop = stop_next;
+        claim = next;
     }
     if (lane == 0) __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -37,6 +37,7 @@ NONCE = [1, 2, 3, 4]
 SWEEP_NTZ = 32
 CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 K0 = 1 << 24                      # start of the L = 4 segment
+PROFILE_TAG = "r01"                # profiles/<tag>_summary.json of the current kernel
 TTS_BATCH_K = 1 << 22              # time-to-secret batches: 2^30 candidates per batch over all ranks
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
 # INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,
@@ -152,6 +153,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_threads, args.cpu_seconds)
 
+    # HBM bytes per sweep launch from the committed rocprofv3 PMC passes of this kernel
+    # (FETCH_SIZE and WRITE_SIZE in separate passes, tools/profile_gpu.sh + tools/summarize_profile.py)
+    traffic, traffic_src = None, None
+    prof = os.path.join(ROOT, "profiles", PROFILE_TAG + "_summary.json")
+    if os.path.exists(prof):
+        ps = json.load(open(prof))
+        if "hbm_bytes_per_launch" in ps:
+            traffic = int(ps["hbm_bytes_per_launch"])
+            traffic_src = f"profiles/{PROFILE_TAG}_summary.json (FETCH_SIZE+WRITE_SIZE per 2^32-candidate launch)"
+
     if rank == 0:
         cus, bpc, tpb = miner.geometry()
         out = {
@@ -181,7 +192,8 @@ def main():
                 "peak": round(PEAK_TOPS, 3),
                 "unit": "TOP/s (INT32 VALU lane-ops)",
                 "frac": round(achieved_tops / PEAK_TOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "ops_per_candidate": OPS_PER_CANDIDATE,
                 "avg_launch_ms": round(avg_launch_ms, 4),
                 "candidates_per_launch": int(cand_per_launch),

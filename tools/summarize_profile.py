@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Summarize a tools/profile_gpu.sh output directory into profiles/<tag>_summary.json.
+
+    python tools/summarize_profile.py gpurun_out/prof_<tag> profiles/<tag>
+
+Writes:
+  <out>_kernel_stats.csv   rocprofv3 --stats table of the bench command (copied)
+  <out>_summary.json       per-kernel averages over the sweep launches (grid of the
+                           2^32-candidate launches), PMC-derived VALU instructions per
+                           candidate, effective clock, and HBM bytes per launch.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def dispatches(path):
+    rows = list(csv.DictReader(open(path)))
+    agg = collections.defaultdict(dict)
+    for r in rows:
+        if "md5_search" not in r["Kernel_Name"]:
+            continue
+        d = agg[r["Dispatch_Id"]]
+        d[r["Counter_Name"]] = float(r["Counter_Value"])
+        d["grid"] = int(r["Grid_Size"])
+        d["ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    return agg
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), out + "_kernel_stats.csv")
+    trace = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
+    sweep = sorted((r for r in trace if "md5_search" in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in sweep]
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    per_step = bench["roofline"]["launches"] // bench["steps"]
+    # bench order: warmup steps, timed steps, then time-to-secret launches
+    timed = dur[bench["warmup"] * per_step:(bench["warmup"] + bench["steps"]) * per_step]
+    big = int(sweep[bench["warmup"] * per_step]["Grid_Size_X"])
+    summary = {
+        "kernel": sweep[0]["Kernel_Name"],
+        "bench_command": "python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe",
+        "timed_sweep_launches": len(timed),
+        "timed_sweep_avg_launch_ms": sum(timed) / len(timed),
+        "bench_avg_launch_ms_hip_events": bench["roofline"]["avg_launch_ms"],
+        "bench_value_ghs": bench["value"],
+        "all_md5_launches_incl_time_to_secret": len(sweep),
+        "all_md5_avg_launch_ms": sum(dur) / len(dur),
+        "sweep_launch_grid_threads": big,
+        "sgpr_count": int(sweep[0]["SGPR_Count"]), "vgpr_count": int(sweep[0]["VGPR_Count"]),
+        "candidates_per_sweep_launch": 1 << 32,
+    }
+    pmc = {}
+    for name in ("pmc_sq", "pmc_fetch", "pmc_write"):
+        p = os.path.join(src, name, "run_counter_collection.csv")
+        if os.path.exists(p):
+            for d in dispatches(p).values():
+                if d["grid"] == big:
+                    for k, v in d.items():
+                        pmc.setdefault(k, []).append(v)
+    if pmc:
+        avg = {k: sum(v) / len(v) for k, v in pmc.items()}
+        n = 1 << 32
+        if "SQ_INSTS_VALU" in avg:
+            summary["valu_insts_per_candidate"] = avg["SQ_INSTS_VALU"] * 64 / n
+            summary["salu_insts_per_candidate"] = avg["SQ_INSTS_SALU"] * 64 / n
+            summary["waves_per_launch"] = avg["SQ_WAVES"]
+            summary["pmc_launch_ms"] = avg["ms"]
+            summary["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / (avg["ms"] * 1e-3) / 1e9
+        if "FETCH_SIZE" in avg:
+            summary["fetch_bytes_per_launch"] = avg["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in avg:
+            summary["write_bytes_per_launch"] = avg["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+            summary["hbm_bytes_per_launch"] = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+    json.dump(summary, open(out + "_summary.json", "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()

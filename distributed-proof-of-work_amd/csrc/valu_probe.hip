@@ -56,7 +56,40 @@ __global__ void __launch_bounds__(kThreads) valu_probe_kernel(uint32_t *out, uin
         for (int u = 0; u < kUnroll; ++u) {
 #pragma unroll
             for (int j = 0; j < kChains; ++j) {
-                if constexpr (KIND == 5) {
+                if constexpr (KIND == 19 || KIND == 20) {
+                    // MD5-step mix interleaved at instruction granularity across chains:
+                    // 19: all 8 chains per instruction; 20: pairs of chains (the NC = 2 shape)
+                    constexpr int G = KIND == 19 ? kChains : 2;
+                    if (j % G == 0) {
+                        uint32_t f[G];
+#pragma unroll
+                        for (int q = 0; q < G; ++q)
+                            asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(f[q]) : "v"(x[j + q]), "v"(b), "v"(c));
+#pragma unroll
+                        for (int q = 0; q < G; ++q)
+                            asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[j + q]) : "v"(f[q]), "v"(c));
+#pragma unroll
+                        for (int q = 0; q < G; ++q) asm volatile("v_alignbit_b32 %0, %0, %0, 25" : "+v"(x[j + q]));
+#pragma unroll
+                        for (int q = 0; q < G; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j + q]) : "v"(b));
+                    }
+                } else if constexpr (KIND == 21) {
+                    // two adds instead of add3, pairs of chains interleaved
+                    if (j % 2 == 0) {
+                        uint32_t f[2];
+#pragma unroll
+                        for (int q = 0; q < 2; ++q)
+                            asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(f[q]) : "v"(x[j + q]), "v"(b), "v"(c));
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j + q]) : "v"(c));
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j + q]) : "v"(f[q]));
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) asm volatile("v_alignbit_b32 %0, %0, %0, 25" : "+v"(x[j + q]));
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j + q]) : "v"(b));
+                    }
+                } else if constexpr (KIND == 5) {
                     uint32_t f = x[j];
                     asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(f) : "v"(x[j]), "v"(b), "v"(c));
                     asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[j]) : "v"(f), "v"(c));
@@ -89,7 +122,7 @@ hipError_t run(uint32_t blocks, uint32_t iters, uint32_t *out, uint64_t *clk, hi
 }  // namespace
 
 extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz) {
-    if (kind < 0 || kind > 18 || !lane_ops_per_s || !clock_ghz) return -1;
+    if (kind < 0 || kind > 21 || !lane_ops_per_s || !clock_ghz) return -1;
     if (hipSetDevice(device) != hipSuccess) return -2;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -2;
@@ -124,7 +157,10 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             case 15: return run<15>(blocks, iters, out, clk, s);
             case 16: return run<16>(blocks, iters, out, clk, s);
             case 17: return run<17>(blocks, iters, out, clk, s);
-            default: return run<18>(blocks, iters, out, clk, s);
+            case 18: return run<18>(blocks, iters, out, clk, s);
+            case 19: return run<19>(blocks, iters, out, clk, s);
+            case 20: return run<20>(blocks, iters, out, clk, s);
+            default: return run<21>(blocks, iters, out, clk, s);
         }
     };
     hipError_t err = hipSuccess;
@@ -145,7 +181,8 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             ratio += (double)h[2 * bI] / (double)h[2 * bI + 1];
             ++n;
         }
-    const double instr_per_lane = (double)iters * kUnroll * kChains * (kind == 5 ? 4 : 1);
+    const double instr_per_lane =
+        (double)iters * kUnroll * kChains * (kind == 5 || kind == 19 || kind == 20 ? 4 : kind == 21 ? 5 : 1);
     *lane_ops_per_s = instr_per_lane * (double)blocks * kThreads * reps / (ms * 1e-3);
     *clock_ghz = n ? ratio / n * 0.1 : 0.0;  // s_memrealtime ticks at 100 MHz
     (void)hipFree(out);

@@ -275,6 +275,13 @@ int dpow_worker_new(int device, dpow_worker **out) {
     *out = new (std::nothrow) dpow_worker();
     if (!*out) return DPOW_ENOMEM;
     (*out)->device = device;
+    // Open one search context up front (stream, control block, pinned flag) so
+    // the first Mine does not pay for it.  Without a visible GPU this is skipped;
+    // a miner then fails its search loudly when it needs one.
+    if (dpow_device_count() > device) {
+        dpow_ctx *c = nullptr;
+        if (dpow_open(device, &c) == 0) (*out)->pool.push_back(c);
+    }
     return 0;
 }
 

@@ -15,7 +15,9 @@ extern "C" {
  *        4 v_fma_f32, 5 the MD5 step mix (bitop3, add3, alignbit, add),
  *        6 v_lshl_add_u32, 7 v_lshl_or_b32, 8 v_xad_u32, 9 v_perm_b32, 10 v_lshlrev_b32,
  *        11 v_or3_b32, 12 v_add_u32 with a literal, 13 v_alignbyte_b32, 14 v_bfi_b32,
- *        15 v_add_lshl_u32, 16 v_xor_b32, 17 v_add3_u32 with an SGPR operand, 18 v_pk_add_u16.
+ *        15 v_add_lshl_u32, 16 v_xor_b32, 17 v_add3_u32 with an SGPR operand, 18 v_pk_add_u16,
+ *        19 the MD5 step mix interleaved across all 8 chains per instruction, 20 the same
+ *        interleaved across pairs of chains, 21 as 20 with two v_add_u32 instead of v_add3_u32.
  * *lane_ops_per_s = wave64 instructions x 64 / s; *clock_ghz = mean in-kernel
  * shader clock (s_memtime / s_memrealtime).  Returns 0, or < 0 on error. */
 int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz);

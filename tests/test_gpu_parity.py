@@ -168,3 +168,35 @@ def test_stats_count_candidates(miner):
     assert r.status == EXHAUSTED
     s = miner.stats()
     assert s.candidates == 4096 * 256 and s.launches == 1 and s.kernel_ms > 0
+
+
+def test_min_over_8_partitions_n8_full_size(miner, golden):
+    """BASELINE config 4 at full size: 8 partitions (workerBits = 3), N = 8; the
+    minimum of the per-partition first hits is the golden workerBits = 0 answer,
+    owned by partition 0."""
+    e = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 8)
+    hits = []
+    for wb in range(8):
+        r = miner.search([1, 2, 3, 4], 8, wb, 3, 0, (e["global_idx"] >> 8) + 1)
+        if r.status == FOUND:
+            assert distpow.verify([1, 2, 3, 4], r.secret, 8)
+            hits.append((r.global_idx, wb))
+    assert min(hits) == (e["global_idx"], 0)
+
+
+def test_native_cli(tmp_path):
+    """The C++ harness (distpow/dpow_cli) drives the C ABI without Python."""
+    import json
+    import os
+    import subprocess
+    cli = os.path.join(os.path.dirname(distpow.LIB_PATH), "dpow_cli")
+    out = json.loads(subprocess.check_output([cli, "mine", "01020304", "7"], timeout=120).decode().strip())
+    assert out["status"] == 1 and out["global_idx"] == 231910082 and out["secret"] == [194, 170, 210, 13]
+    assert out["verified"] == 1
+    out = json.loads(subprocess.check_output([cli, "mine", "01020304", "6", "2", "2"], timeout=120).decode())
+    assert out["secret"] == [188, 163, 38]
+    out = json.loads(subprocess.check_output([cli, "worker", "05060708", "5"], timeout=120).decode())
+    assert out["secret"] == [84, 244, 3] and out["ack_is_nil"] == 1
+    out = json.loads(subprocess.check_output([cli, "sweep", "32"], timeout=120).decode())
+    assert out["status"] == 0 and out["candidates"] == 1 << 32
+    print("cli sweep", out)

@@ -85,8 +85,12 @@ def main():
     dev = torch.device("cuda", device) if args.backend == "nccl" else torch.device("cpu")
     red = torch.empty(2, dtype=torch.int64, device=dev)
 
+    # Every step's window stays inside the L = 4 chunk segment [2^24, 2^32): at N = 8 a
+    # step is 2^31 k per rank, so windows cycle over the segment's whole windows.
+    n_windows = ((1 << 32) - K0) // batch_k
+
     def step(s):
-        k_begin = K0 + s * batch_k
+        k_begin = K0 + (s % n_windows) * batch_k
         r = miner.search(NONCE, SWEEP_NTZ, wb, wbits, k_begin, k_begin + batch_k)
         assert r.status == distpow.EXHAUSTED, r  # N = 32 is unreachable in 2^36 candidates
         if world > 1:

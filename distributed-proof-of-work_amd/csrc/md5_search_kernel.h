@@ -32,6 +32,9 @@ namespace dpow {
 // SGPR budget: <= 80 allocated SGPRs admit 8 four-wave workgroups per CU
 // (8 waves per SIMD, MI355X_MICROARCH.md "Residency").  Literal K constants are
 // rematerialised by SALU moves, which co-issue beside other waves' VALU.
+#ifndef DPOW_FOLD_ZERO
+#define DPOW_FOLD_ZERO 1  // fold always-zero message words to literal K (A/B switch)
+#endif
 #ifndef DPOW_ADD_MODE
 #define DPOW_ADD_MODE 0  // 0: compiler's choice (v_add3_u32); 1: two VOP2 v_add_u32
 #endif
@@ -62,7 +65,7 @@ DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &
         // Words past the variable bytes, the chunk tail and the 0x80 pad -- every
         // word after W0 + 2 except the bit-length word -- are zero for every launch
         // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
-        constexpr bool zero_word = m > W0 + 2 && m != 16 * NBLK - 2;
+        constexpr bool zero_word = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
         const uint32_t kt = zero_word ? kMd5K[I] : L.KT[64 * BLK + I];
 #pragma unroll
         for (int j = 0; j < NCAND; ++j) {

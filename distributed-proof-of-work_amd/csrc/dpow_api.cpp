@@ -53,7 +53,7 @@ constexpr size_t kClaimRing = 1024;  // per-launch claim counters, zeroed per se
 // snapshot behind launch j - kDepth shows no hit and no cancel, so a hit or a
 // cancel leaves at most kDepth launches to retire (each exits at its first check).
 constexpr size_t kDepth = 3;
-constexpr size_t kRing = 8;  // pinned control-block snapshots (>= kDepth + 1)
+constexpr size_t kRing = 8;  // pinned control-block snapshots and event slots (>= kDepth + 1)
 
 }  // namespace
 
@@ -66,9 +66,8 @@ struct dpow_ctx {
     uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped
     uint32_t *d_cancel = nullptr;  // device alias
     uint32_t cus = 0;
-    std::vector<hipEvent_t> events;  // 2 per launch of the last search
+    std::vector<hipEvent_t> events;  // 3 per ring slot: start, kernel end, snapshot landed
     dpow_stats stats{};
-    std::vector<PlannedLaunch> plan;
 };
 
 extern "C" {
@@ -210,35 +209,47 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     if (k_begin >= k_end) return DPOW_EXHAUSTED;
     if (__atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
 
-    int n = plan_window(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end, c->plan);
-    if (n < 0) return set_error(n, "dpow_search: planning failed");
+    WindowPlanner planner;
+    int rc = planner.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
+    if (rc < 0) return set_error(rc, "dpow_search: planning failed");
     DPOW_HIP(hipSetDevice(c->device));
+    while (c->events.size() < 3 * kRing) {  // {start, kernel end, snapshot landed} per ring slot
+        hipEvent_t ev;
+        DPOW_HIP(hipEventCreate(&ev));
+        c->events.push_back(ev);
+    }
+    auto ev = [&](size_t li, int which) { return c->events[3 * (li % kRing) + which]; };
 
     const uint64_t bound = *best_global_idx;
     c->h_ctrl->best = bound;
     c->h_ctrl->stop = 0;
     c->h_ctrl->done = 0;
     DPOW_HIP(hipMemcpyAsync(c->d_ctrl, c->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, c->stream));
-
-    while (c->events.size() < 2 * c->plan.size()) {
-        hipEvent_t ev;
-        DPOW_HIP(hipEventCreate(&ev));
-        c->events.push_back(ev);
-    }
+    DPOW_HIP(hipMemsetAsync(c->d_claims, 0, kClaimRing * sizeof(unsigned long long), c->stream));
 
     constexpr uint32_t wpb = kBlockThreads / 64;
-    const size_t nz = c->plan.size() < kClaimRing ? c->plan.size() : kClaimRing;
-    DPOW_HIP(hipMemsetAsync(c->d_claims, 0, nz * sizeof(unsigned long long), c->stream));
     uint32_t done_target = 0;
     uint64_t candidates = 0;
-    size_t launched = 0;
-    for (size_t li = 0; li < c->plan.size(); ++li) {
-        if (li >= kDepth) {  // look at the snapshot behind launch li - kDepth
-            DPOW_HIP(hipEventSynchronize(c->events[2 * (li - kDepth) + 1]));
-            const Ctrl &snap = c->h_ctrl[1 + (li - kDepth) % kRing];
+    double ms_total = 0.0;
+    size_t launched = 0, retired = 0;
+    // Kernel time of a launch whose snapshot has landed (its events are complete).
+    auto retire = [&](size_t li) -> int {
+        float ms = 0.f;
+        DPOW_HIP(hipEventElapsedTime(&ms, ev(li, 0), ev(li, 1)));
+        ms_total += ms;
+        return 0;
+    };
+    PlannedLaunch pl;
+    while (planner.next(pl)) {
+        const size_t li = launched;
+        if (li >= kDepth) {  // the snapshot behind launch li - kDepth decides whether to go on
+            const size_t lj = li - kDepth;
+            DPOW_HIP(hipEventSynchronize(ev(lj, 2)));
+            if (retire(lj) < 0) return DPOW_EHIP;
+            retired = lj + 1;
+            const Ctrl &snap = c->h_ctrl[1 + lj % kRing];
             if (snap.best < bound || snap.stop != 0u || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) break;
         }
-        PlannedLaunch &pl = c->plan[li];
         Launch &L = pl.L;
         unsigned long long *claim = c->d_claims + li % kClaimRing;
         if (li >= kClaimRing) DPOW_HIP(hipMemsetAsync(claim, 0, sizeof(unsigned long long), c->stream));
@@ -254,25 +265,21 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;
         L.cancel = c->d_cancel;
-        DPOW_HIP(hipEventRecord(c->events[2 * li], c->stream));
+        DPOW_HIP(hipEventRecord(ev(li, 0), c->stream));
         hipError_t e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L,
                                      (uint32_t)(worker_blocks + 1), c->stream);
         if (e != hipSuccess) return hip_fail(e, "search_launch");
+        DPOW_HIP(hipEventRecord(ev(li, 1), c->stream));
         DPOW_HIP(hipMemcpyAsync(&c->h_ctrl[1 + li % kRing], c->d_ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost,
                                 c->stream));
-        DPOW_HIP(hipEventRecord(c->events[2 * li + 1], c->stream));
+        DPOW_HIP(hipEventRecord(ev(li, 2), c->stream));
         candidates += L.i_end - L.i_begin;
         ++launched;
     }
     DPOW_HIP(hipStreamSynchronize(c->stream));
+    for (size_t lj = retired; lj < launched; ++lj)
+        if (retire(lj) < 0) return DPOW_EHIP;
     const Ctrl fin = c->h_ctrl[1 + (launched - 1) % kRing];
-
-    double ms_total = 0.0;
-    for (size_t li = 0; li < launched; ++li) {
-        float ms = 0.f;
-        DPOW_HIP(hipEventElapsedTime(&ms, c->events[2 * li], c->events[2 * li + 1]));
-        ms_total += ms;
-    }
     c->stats.launches += launched;
     c->stats.candidates += candidates;
     c->stats.kernel_ms += ms_total;

@@ -37,67 +37,81 @@ uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits) {
     return (uint32_t)((worker_byte << remainder_bits(worker_bits)) & 0xFFu);
 }
 
+int WindowPlanner::init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
+                        uint32_t worker_bits, uint64_t k_begin, uint64_t k_end) {
+    if (nonce_len && !nonce) return -1;
+    if (worker_byte > 255u) return -1;
+    if (k_end > (1ull << 40)) return -4;
+    nonce_ = nonce;
+    nonce_len_ = nonce_len;
+    ntz_ = ntz;
+    rbits_ = remainder_bits(worker_bits);
+    base_tb_ = base_thread_byte(worker_byte, worker_bits);
+    blk_v_ = nonce_len / 64;  // first block holding variable bytes
+    p_ = (uint32_t)(nonce_len % 64);
+    k_ = k_begin;
+    k_end_ = k_end;
+    // Midstate over nonce-only blocks.
+    for (int w = 0; w < 4; ++w) iv_[w] = kMd5IV[w];
+    for (size_t b = 0; b < blk_v_; ++b) {
+        uint32_t M[16];
+        for (int w = 0; w < 16; ++w) M[w] = load_le32(nonce + 64 * b + 4 * w);
+        md5_compress(iv_, M);
+    }
+    return 0;
+}
+
+bool WindowPlanner::next(PlannedLaunch &pl) {
+    if (k_ >= k_end_) return false;
+    const uint64_t k = k_;
+    const uint64_t ke = segment_end(k) < k_end_ ? segment_end(k) : k_end_;
+    const uint32_t L = chunk_len_of(k);
+    const size_t msg_len = nonce_len_ + 1 + L;
+    const size_t total_blocks = (msg_len + 8) / 64 + 1;
+    const uint32_t nblk = (uint32_t)(total_blocks - blk_v_);
+    memset(&pl, 0, sizeof pl);
+    Launch &Lh = pl.L;
+    uint8_t buf[128];
+    memset(buf, 0, sizeof buf);
+    const uint32_t p = p_;
+    if (p) memcpy(buf, nonce_ + 64 * blk_v_, p);
+    // buf[p] = threadByte and buf[p+1 .. p+min(L,3)] = low chunk bytes: variable (left 0).
+    for (uint32_t j = 3; j < L; ++j) buf[p + 1 + j] = (uint8_t)(k >> (8 * j));
+    buf[p + 1 + L] = 0x80;
+    const uint64_t bits = (uint64_t)msg_len * 8u;
+    for (int j = 0; j < 8; ++j) buf[64 * nblk - 8 + j] = (uint8_t)(bits >> (8 * j));
+    for (int w = 0; w < 4; ++w) Lh.iv[w] = iv_[w];
+    for (uint32_t w = 0; w < 16 * nblk; ++w) Lh.T[w] = load_le32(buf + 4 * w);
+    for (uint32_t b = 0; b < nblk; ++b)
+        for (int s = 0; s < 64; ++s) Lh.KT[64 * b + s] = kMd5K[s] + Lh.T[16 * b + md5_word(s)];
+    Lh.i_begin = k << rbits_;
+    Lh.i_end = ke << rbits_;
+    Lh.wb_begin = Lh.i_begin & ~63ull;
+    Lh.n_wblocks = (Lh.i_end - Lh.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
+    Lh.rbits = rbits_;
+    Lh.base_tb = base_tb_;
+    Lh.dmask = tail_nibble_mask(ntz_ < 8 ? ntz_ : 8);
+    Lh.ntz = ntz_;
+    pl.info.k_begin = k;
+    pl.info.k_end = ke;
+    pl.info.i_begin = Lh.i_begin;
+    pl.info.i_end = Lh.i_end;
+    pl.info.nblk = nblk;
+    pl.info.w0 = p / 4;
+    pl.info.sh = p % 4;
+    pl.info.chunk_len = L;
+    k_ = ke;
+    return true;
+}
+
 int plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
                 uint32_t worker_bits, uint64_t k_begin, uint64_t k_end, std::vector<PlannedLaunch> &out) {
     out.clear();
-    if (nonce_len && !nonce) return -1;
-    if (worker_byte > 255u) return -1;
-    if (k_begin >= k_end) return 0;
-    if (k_end > (1ull << 40)) return -4;
-    const uint32_t rbits = remainder_bits(worker_bits);
-    const uint32_t base_tb = base_thread_byte(worker_byte, worker_bits);
-    const size_t blk_v = nonce_len / 64;  // first block holding variable bytes
-    const uint32_t p = (uint32_t)(nonce_len % 64);
-
-    // Midstate over nonce-only blocks.
-    uint32_t iv[4] = {kMd5IV[0], kMd5IV[1], kMd5IV[2], kMd5IV[3]};
-    for (size_t b = 0; b < blk_v; ++b) {
-        uint32_t M[16];
-        for (int w = 0; w < 16; ++w) M[w] = load_le32(nonce + 64 * b + 4 * w);
-        md5_compress(iv, M);
-    }
-
-    uint64_t k = k_begin;
-    while (k < k_end) {
-        const uint64_t ke = segment_end(k) < k_end ? segment_end(k) : k_end;
-        const uint32_t L = chunk_len_of(k);
-        const size_t msg_len = nonce_len + 1 + L;
-        const size_t total_blocks = (msg_len + 8) / 64 + 1;
-        const uint32_t nblk = (uint32_t)(total_blocks - blk_v);
-        PlannedLaunch pl;
-        memset(&pl, 0, sizeof pl);
-        Launch &Lh = pl.L;
-        uint8_t buf[128];
-        memset(buf, 0, sizeof buf);
-        if (p) memcpy(buf, nonce + 64 * blk_v, p);
-        // buf[p] = threadByte and buf[p+1 .. p+min(L,3)] = low chunk bytes: variable (left 0).
-        for (uint32_t j = 3; j < L; ++j) buf[p + 1 + j] = (uint8_t)(k >> (8 * j));
-        buf[p + 1 + L] = 0x80;
-        const uint64_t bits = (uint64_t)msg_len * 8u;
-        for (int j = 0; j < 8; ++j) buf[64 * nblk - 8 + j] = (uint8_t)(bits >> (8 * j));
-        for (int w = 0; w < 4; ++w) Lh.iv[w] = iv[w];
-        for (uint32_t w = 0; w < 16 * nblk; ++w) Lh.T[w] = load_le32(buf + 4 * w);
-        for (uint32_t b = 0; b < nblk; ++b)
-            for (int s = 0; s < 64; ++s) Lh.KT[64 * b + s] = kMd5K[s] + Lh.T[16 * b + md5_word(s)];
-        Lh.i_begin = k << rbits;
-        Lh.i_end = ke << rbits;
-        Lh.wb_begin = Lh.i_begin & ~63ull;
-        Lh.n_wblocks = (Lh.i_end - Lh.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
-        Lh.rbits = rbits;
-        Lh.base_tb = base_tb;
-        Lh.dmask = tail_nibble_mask(ntz < 8 ? ntz : 8);
-        Lh.ntz = ntz;
-        pl.info.k_begin = k;
-        pl.info.k_end = ke;
-        pl.info.i_begin = Lh.i_begin;
-        pl.info.i_end = Lh.i_end;
-        pl.info.nblk = nblk;
-        pl.info.w0 = p / 4;
-        pl.info.sh = p % 4;
-        pl.info.chunk_len = L;
-        out.push_back(pl);
-        k = ke;
-    }
+    WindowPlanner wp;
+    int rc = wp.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
+    if (rc < 0) return rc;
+    PlannedLaunch pl;
+    while (wp.next(pl)) out.push_back(pl);
     return (int)out.size();
 }
 

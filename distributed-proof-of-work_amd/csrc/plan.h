@@ -12,13 +12,29 @@ namespace dpow {
 
 struct PlannedLaunch {
     dpow_plan_launch info;
-    Launch L;  // ctrl / cancel / done_target / iters filled at launch time
+    Launch L;  // ctrl / cancel / claim / chunk / done_target filled at launch time
 };
 
 uint32_t chunk_len_of(uint64_t k);
 uint64_t segment_end(uint64_t k);
 uint32_t remainder_bits(uint32_t worker_bits);
 uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits);
+
+// Incremental planner: one launch at a time, so a window of any size costs
+// O(1) host memory.  init() returns 0 or a negative DPOW_E* code.
+class WindowPlanner {
+   public:
+    int init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte, uint32_t worker_bits,
+             uint64_t k_begin, uint64_t k_end);
+    bool next(PlannedLaunch &out);  // false when the window is covered
+
+   private:
+    const uint8_t *nonce_ = nullptr;
+    size_t nonce_len_ = 0, blk_v_ = 0;
+    uint32_t p_ = 0, ntz_ = 0, rbits_ = 0, base_tb_ = 0;
+    uint64_t k_ = 0, k_end_ = 0;
+    uint32_t iv_[4] = {0, 0, 0, 0};
+};
 
 // Returns the number of launches, or a negative DPOW_E* code.
 int plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,

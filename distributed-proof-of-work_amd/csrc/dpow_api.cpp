@@ -2,14 +2,20 @@
 //
 // dpow_search replaces the reference miner's enumeration loop
 // (worker.go:301-400): plan the window into launches (plan.cpp), queue them on
-// the context's stream behind one control-block reset with at most kDepth in
-// flight (a pinned snapshot of the control block follows each launch), and
-// re-verify a hit with the host MD5 before returning it.  Launches queued after
-// a hit (or a cancel) retire at once: every worker wave compares its first
-// index against Ctrl::best / Ctrl::stop before hashing.
+// the context's stream behind one reset kernel with at most kDepth in flight,
+// and re-verify a hit with the host MD5 before returning it.  Each launch's
+// last retiring workgroup writes a completion record (the control block as of
+// the end of the launch) to pinned host memory; the host polls that record rather
+// than synchronising on events, so a hit is seen one PCIe write after the
+// kernel publishes it.  Launches queued behind a hit (or a cancel) are not
+// waited for: they retire at once (every worker wave compares its first index
+// against Ctrl::best / Ctrl::stop before hashing), in stream order ahead of
+// the next search on the context.
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <time.h>
 
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -49,11 +55,23 @@ constexpr uint64_t kBlocksPerCu = 8;
 constexpr uint64_t kClaimsPerWave = 16;
 constexpr uint64_t kMaxChunk = 32;
 constexpr size_t kClaimRing = 1024;  // per-launch claim counters, zeroed per search
-// Launches kept in flight: launch j is queued only after the control block
-// snapshot behind launch j - kDepth shows no hit and no cancel, so a hit or a
-// cancel leaves at most kDepth launches to retire (each exits at its first check).
+// Launches kept in flight: launch j is queued only after the completion record
+// of launch j - kDepth shows no hit and no cancel, so a hit or a cancel leaves
+// at most kDepth launches to retire (each exits at its first check).
 constexpr size_t kDepth = 3;
-constexpr size_t kRing = 8;  // pinned control-block snapshots and event slots (>= kDepth + 1)
+constexpr size_t kRing = 8;  // completion records and event pairs, indexed by launch seq (>= kDepth + 1)
+// Completion-record wait: spin this long (time-to-secret), then poll at kPollNs.
+constexpr int64_t kSpinNs = 200000;
+constexpr long kPollNs = 20000;
+
+// Timing of one queued launch (its HIP events), harvested into dpow_stats
+// lazily -- never on the path between a hit and dpow_search returning.
+struct LaunchSlot {
+    hipEvent_t start = nullptr, end = nullptr;
+    bool pending = false;  // events recorded, not yet harvested
+    bool counted = false;  // its completion record was consumed: its work counts in the stats
+    uint64_t candidates = 0;
+};
 
 }  // namespace
 
@@ -62,13 +80,70 @@ struct dpow_ctx {
     hipStream_t stream = nullptr;
     Ctrl *d_ctrl = nullptr;
     unsigned long long *d_claims = nullptr;  // kClaimRing claim counters
-    Ctrl *h_ctrl = nullptr;        // pinned staging: [0] reset image, [1 + j % kRing] snapshots
+    Snap *h_snap = nullptr;        // kRing completion records: pinned, host-coherent, mapped
+    Snap *d_snap = nullptr;        // device alias
     uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped
     uint32_t *d_cancel = nullptr;  // device alias
     uint32_t cus = 0;
-    std::vector<hipEvent_t> events;  // 3 per ring slot: start, kernel end, snapshot landed
+    uint64_t seq = 0;  // launches ever queued on this context (record/slot index = seq % kRing)
+    LaunchSlot slots[kRing];
     dpow_stats stats{};
 };
+
+namespace {
+
+// Fold one launch's kernel time into the stats.  Its end event is long
+// complete by the time a slot is reused, so the synchronisation is immediate.
+int harvest(dpow_ctx *c, LaunchSlot &s) {
+    if (!s.pending) return 0;
+    s.pending = false;
+    DPOW_HIP(hipEventSynchronize(s.end));
+    if (!s.counted) return 0;
+    float ms = 0.f;
+    DPOW_HIP(hipEventElapsedTime(&ms, s.start, s.end));
+    c->stats.launches++;
+    c->stats.candidates += s.candidates;
+    c->stats.kernel_ms += ms;
+    return 0;
+}
+
+int harvest_all(dpow_ctx *c) {
+    for (LaunchSlot &s : c->slots)
+        if (harvest(c, s) < 0) return DPOW_EHIP;
+    return 0;
+}
+
+// Wait for the completion record of launch `seq`.  Spins first (the record of
+// a launch holding a hit is the time-to-secret path), then sleeps between
+// polls; the stream is queried now and then so a failed launch, or a stream
+// that went idle without writing the record, ends the wait with an error.
+int wait_record(dpow_ctx *c, uint64_t seq) {
+    const uint32_t *p = &c->h_snap[seq % kRing].seq;
+    const uint32_t want = (uint32_t)(seq + 1);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t it = 1;; ++it) {
+        if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 0;
+        const int64_t ns =
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        const bool spinning = ns < kSpinNs;
+        if (spinning ? (it % 4096 == 0) : (it % 16 == 0)) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 0;
+                return set_error(DPOW_EHIP, "dpow_search: stream idle without the launch's completion record");
+            }
+            if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
+        }
+        if (spinning) {
+            __builtin_ia32_pause();
+        } else {
+            const struct timespec ts = {0, kPollNs};
+            nanosleep(&ts, nullptr);
+        }
+    }
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -104,13 +179,22 @@ int dpow_open(int device, dpow_ctx **out) {
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&c->d_ctrl, sizeof(Ctrl))) != hipSuccess ||
         (e = hipMalloc(&c->d_claims, kClaimRing * sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_ctrl, (1 + kRing) * sizeof(Ctrl), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_snap, kRing * sizeof(Snap), hipHostMallocCoherent | hipHostMallocMapped)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_snap), c->h_snap, 0)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_cancel, 64, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_cancel), c->h_cancel, 0)) != hipSuccess) {
         dpow_close(c);
         return hip_fail(e, "dpow_open: allocation");
     }
+    memset(c->h_snap, 0, kRing * sizeof(Snap));
     memset(c->h_cancel, 0, 64);
+    for (LaunchSlot &s : c->slots) {
+        if ((e = hipEventCreate(&s.start)) != hipSuccess || (e = hipEventCreate(&s.end)) != hipSuccess) {
+            dpow_close(c);
+            return hip_fail(e, "dpow_open: hipEventCreate");
+        }
+    }
     *out = c;
     return 0;
 }
@@ -119,10 +203,13 @@ void dpow_close(dpow_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
+    for (LaunchSlot &s : c->slots) {
+        if (s.start) (void)hipEventDestroy(s.start);
+        if (s.end) (void)hipEventDestroy(s.end);
+    }
     if (c->d_ctrl) (void)hipFree(c->d_ctrl);
     if (c->d_claims) (void)hipFree(c->d_claims);
-    if (c->h_ctrl) (void)hipHostFree(c->h_ctrl);
+    if (c->h_snap) (void)hipHostFree(c->h_snap);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -142,12 +229,15 @@ int dpow_geometry(dpow_ctx *c, uint32_t *cus, uint32_t *blocks_per_cu, uint32_t 
 
 int dpow_get_stats(dpow_ctx *c, dpow_stats *out) {
     if (!c || !out) return set_error(DPOW_EINVAL, "dpow_get_stats: NULL argument");
+    if (harvest_all(c) < 0) return DPOW_EHIP;
     *out = c->stats;
     return 0;
 }
 
 void dpow_reset_stats(dpow_ctx *c) {
-    if (c) c->stats = dpow_stats{};
+    if (!c) return;
+    (void)harvest_all(c);  // launches queued before the reset stay out of the new counts
+    c->stats = dpow_stats{};
 }
 
 int dpow_secret_from_index(uint64_t g, uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len) {
@@ -213,89 +303,95 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     int rc = planner.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
     if (rc < 0) return set_error(rc, "dpow_search: planning failed");
     DPOW_HIP(hipSetDevice(c->device));
-    while (c->events.size() < 3 * kRing) {  // {start, kernel end, snapshot landed} per ring slot
-        hipEvent_t ev;
-        DPOW_HIP(hipEventCreate(&ev));
-        c->events.push_back(ev);
-    }
-    auto ev = [&](size_t li, int which) { return c->events[3 * (li % kRing) + which]; };
 
     const uint64_t bound = *best_global_idx;
-    c->h_ctrl->best = bound;
-    c->h_ctrl->stop = 0;
-    c->h_ctrl->done = 0;
-    DPOW_HIP(hipMemcpyAsync(c->d_ctrl, c->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, c->stream));
-    DPOW_HIP(hipMemsetAsync(c->d_claims, 0, kClaimRing * sizeof(unsigned long long), c->stream));
+    hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)kClaimRing, bound, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "search_reset");
 
     constexpr uint32_t wpb = kBlockThreads / 64;
+    const uint64_t seq0 = c->seq;
     uint32_t done_target = 0;
-    uint64_t candidates = 0;
-    double ms_total = 0.0;
-    size_t launched = 0, retired = 0;
-    // Kernel time of a launch whose snapshot has landed (its events are complete).
-    auto retire = [&](size_t li) -> int {
-        float ms = 0.f;
-        DPOW_HIP(hipEventElapsedTime(&ms, ev(li, 0), ev(li, 1)));
-        ms_total += ms;
-        return 0;
+    size_t launched = 0, consumed = 0;
+    uint64_t best = bound;
+    int status = DPOW_EXHAUSTED;
+    // Consume the completion record of launch lj (in launch order): FOUND or
+    // CANCELLED ends the search, EXHAUSTED goes on, < 0 is an error.  Ctrl::best
+    // persists across the launches of a search and later launches hold higher
+    // indices, so the first record below the bound carries the answer.
+    auto consume = [&](size_t lj) -> int {
+        const uint64_t seq = seq0 + lj;
+        const int rc = wait_record(c, seq);
+        if (rc < 0) return rc;
+        c->slots[seq % kRing].counted = true;
+        consumed = lj + 1;
+        const Snap &sn = c->h_snap[seq % kRing];
+        if (sn.best < bound) {
+            best = sn.best;
+            return DPOW_FOUND;
+        }
+        if (sn.stop != 0u || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
+        return DPOW_EXHAUSTED;
     };
     PlannedLaunch pl;
-    while (planner.next(pl)) {
+    while (status == DPOW_EXHAUSTED && planner.next(pl)) {
         const size_t li = launched;
-        if (li >= kDepth) {  // the snapshot behind launch li - kDepth decides whether to go on
-            const size_t lj = li - kDepth;
-            DPOW_HIP(hipEventSynchronize(ev(lj, 2)));
-            if (retire(lj) < 0) return DPOW_EHIP;
-            retired = lj + 1;
-            const Ctrl &snap = c->h_ctrl[1 + lj % kRing];
-            if (snap.best < bound || snap.stop != 0u || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) break;
+        if (li >= kDepth) {  // the record of launch li - kDepth decides whether to go on
+            const int r = consume(li - kDepth);
+            if (r < 0) return r;
+            if (r != DPOW_EXHAUSTED) {
+                status = r;
+                break;
+            }
         }
+        const uint64_t seq = seq0 + li;
+        LaunchSlot &slot = c->slots[seq % kRing];
+        if (harvest(c, slot) < 0) return DPOW_EHIP;  // the slot's previous launch
         Launch &L = pl.L;
         unsigned long long *claim = c->d_claims + li % kClaimRing;
-        if (li >= kClaimRing) DPOW_HIP(hipMemsetAsync(claim, 0, sizeof(unsigned long long), c->stream));
+        if (li >= kClaimRing) {
+            e = search_reset(nullptr, claim, 1u, 0ull, c->stream);
+            if (e != hipSuccess) return hip_fail(e, "search_reset");
+        }
         uint64_t worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
         if (worker_blocks > (uint64_t)c->cus * kBlocksPerCu) worker_blocks = (uint64_t)c->cus * kBlocksPerCu;
         uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
         if (chunk < 1) chunk = 1;
         if (chunk > kMaxChunk) chunk = kMaxChunk;
-        done_target += (uint32_t)(worker_blocks * wpb);
+        done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.chunk = (uint32_t)chunk;
         L.n_chunks = (L.n_wblocks + chunk - 1) / chunk;
         L.claim = claim;
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;
         L.cancel = c->d_cancel;
-        DPOW_HIP(hipEventRecord(ev(li, 0), c->stream));
-        hipError_t e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L,
-                                     (uint32_t)(worker_blocks + 1), c->stream);
+        L.snap = c->d_snap + seq % kRing;
+        L.seq = (uint32_t)(seq + 1);
+        DPOW_HIP(hipEventRecord(slot.start, c->stream));
+        e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L, (uint32_t)(worker_blocks + 1),
+                          c->stream);
         if (e != hipSuccess) return hip_fail(e, "search_launch");
-        DPOW_HIP(hipEventRecord(ev(li, 1), c->stream));
-        DPOW_HIP(hipMemcpyAsync(&c->h_ctrl[1 + li % kRing], c->d_ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost,
-                                c->stream));
-        DPOW_HIP(hipEventRecord(ev(li, 2), c->stream));
-        candidates += L.i_end - L.i_begin;
+        DPOW_HIP(hipEventRecord(slot.end, c->stream));
+        slot.pending = true;
+        slot.counted = false;
+        slot.candidates = L.i_end - L.i_begin;
+        c->seq = seq + 1;
         ++launched;
     }
-    DPOW_HIP(hipStreamSynchronize(c->stream));
-    for (size_t lj = retired; lj < launched; ++lj)
-        if (retire(lj) < 0) return DPOW_EHIP;
-    const Ctrl fin = c->h_ctrl[1 + (launched - 1) % kRing];
-    c->stats.launches += launched;
-    c->stats.candidates += candidates;
-    c->stats.kernel_ms += ms_total;
+    while (status == DPOW_EXHAUSTED && consumed < launched) {  // the window is queued: drain in order
+        const int r = consume(consumed);
+        if (r < 0) return r;
+        status = r;
+    }
 
-    const uint64_t best = fin.best;
-    if (best < bound) {
+    if (status == DPOW_FOUND) {
         dpow_secret_from_index(best, secret_out, secret_len);
         if (!dpow_verify(nonce, nonce_len, secret_out, *secret_len, ntz)) {
             *secret_len = 0;
             return set_error(DPOW_EVERIFY, "dpow_search: kernel hit failed host MD5 verification");
         }
         *best_global_idx = best;
-        return DPOW_FOUND;
     }
-    if (fin.stop != 0u || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
-    return DPOW_EXHAUSTED;
+    return status;
 }
 
 }  // extern "C"

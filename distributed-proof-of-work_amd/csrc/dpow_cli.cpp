@@ -4,6 +4,9 @@
 //       the reference miner's answer for one partition (worker.go:301-400), verified on the host
 //   dpow_cli sweep <log2-candidates> [device]
 //       hash 2^n candidates of nonce 01020304 at N=32 (unreachable) from k = 2^24, report GH/s
+//   dpow_cli latency [reps [device]]
+//       time-to-secret floor: platform launch round trips (dpow_diag.h) and median dpow_search
+//       latency for hits at N = 0 / 3 / 5 (in-process, warm context)
 //   dpow_cli worker <nonce-hex> <ntz> [device]
 //       one Mine -> result -> Found -> ACK round trip through the native worker (worker.go:169-232)
 // Each command prints one JSON line.
@@ -15,7 +18,10 @@
 #include <string>
 #include <vector>
 
+#include <algorithm>
+
 #include "../../include/dpow.h"
+#include "../../include/dpow_diag.h"
 #include "../../include/dpow_worker.h"
 
 static std::vector<uint8_t> from_hex(const char *s) {
@@ -102,6 +108,51 @@ static int cmd_sweep(int argc, char **argv) {
     return 0;
 }
 
+static int cmd_latency(int argc, char **argv) {
+    const int reps = argc > 2 ? atoi(argv[2]) : 200;
+    const int dev = argc > 3 ? atoi(argv[3]) : 0;
+    double floor_us[3] = {0, 0, 0};
+    for (int m = 0; m < 3; ++m)
+        if (dpow_diag_launch_latency(dev, m, reps, &floor_us[m]) != 0) return fail("dpow_diag_launch_latency", -2);
+    dpow_ctx *ctx = nullptr;
+    int rc = dpow_open(dev, &ctx);
+    if (rc) return fail("dpow_open", rc);
+    const uint8_t nonce[4] = {1, 2, 3, 4};
+    const uint8_t nonce5[4] = {2, 2, 2, 2};
+    struct Case { const uint8_t *n; uint32_t ntz; uint64_t k_end; const char *name; int idle_us; } cases[] = {
+        {nonce, 0, 1, "n0_k1", 0},           {nonce, 3, 1, "n3_k1", 0},
+        {nonce, 3, 256, "n3_k256", 0},       {nonce, 3, 65536, "n3_k64k", 0},
+        {nonce, 3, 1ull << 24, "n3_k16M", 0}, {nonce, 3, 1ull << 26, "n3", 0},
+        {nonce, 3, 1ull << 26, "n3_idle", 3000}, {nonce5, 5, 1ull << 26, "n5_02020202", 0},
+        {nonce5, 5, 1ull << 26, "n5_02020202_idle", 3000}};
+    std::string out = "{\"launch_sync_us\":" + std::to_string(floor_us[0]) +
+                      ",\"launch_pinned_poll_us\":" + std::to_string(floor_us[1]) +
+                      ",\"memcpy16_d2h_sync_us\":" + std::to_string(floor_us[2]);
+    for (const Case &c : cases) {
+        std::vector<double> us;
+        for (int r = 0; r < reps + 5; ++r) {
+            uint64_t best = DPOW_NO_HIT;
+            uint8_t secret[DPOW_MAX_SECRET];
+            size_t slen = 0;
+            if (c.idle_us) {  // let the previous search's queued launches drain first
+                const double tw = now_s();
+                while ((now_s() - tw) * 1e6 < c.idle_us) {
+                }
+            }
+            const double t0 = now_s();
+            rc = dpow_search(ctx, c.n, 4, c.ntz, 0, 0, 0, c.k_end, &best, secret, &slen);
+            const double dt = (now_s() - t0) * 1e6;
+            if (rc != DPOW_FOUND) return fail("dpow_search", rc);
+            if (r >= 5) us.push_back(dt);
+        }
+        std::sort(us.begin(), us.end());
+        out += std::string(",\"search_") + c.name + "_us\":" + std::to_string(us[us.size() / 2]);
+    }
+    dpow_close(ctx);
+    printf("%s}\n", out.c_str());
+    return 0;
+}
+
 static int cmd_worker(int argc, char **argv) {
     if (argc < 4) return 2;
     std::vector<uint8_t> nonce = from_hex(argv[2]);
@@ -132,9 +183,11 @@ int main(int argc, char **argv) {
     if (argc >= 2 && !strcmp(argv[1], "mine")) return cmd_mine(argc, argv);
     if (argc >= 2 && !strcmp(argv[1], "sweep")) return cmd_sweep(argc, argv);
     if (argc >= 2 && !strcmp(argv[1], "worker")) return cmd_worker(argc, argv);
+    if (argc >= 2 && !strcmp(argv[1], "latency")) return cmd_latency(argc, argv);
     fprintf(stderr,
             "usage: dpow_cli mine <nonce-hex> <ntz> [worker_byte worker_bits [device]]\n"
             "       dpow_cli sweep <log2-candidates> [device]\n"
-            "       dpow_cli worker <nonce-hex> <ntz> [device]\n");
+            "       dpow_cli worker <nonce-hex> <ntz> [device]\n"
+            "       dpow_cli latency [reps [device]]\n");
     return 2;
 }

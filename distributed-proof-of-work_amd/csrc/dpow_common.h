@@ -59,7 +59,17 @@ constexpr int kBlockThreads = 256;    // 4 waves per workgroup
 struct Ctrl {
     unsigned long long best;  // min global index found (DPOW_NO_HIT = none), atomicMin target
     uint32_t stop;            // set by the watcher when the host cancel flag is raised
-    uint32_t done;            // worker waves retired (cumulative within one search)
+    uint32_t done;            // worker workgroups retired (cumulative within one search)
+};
+
+// Host-visible completion record of one launch (pinned, host-coherent, mapped).
+// The launch's last retiring workgroup writes it: the
+// control block as of the end of the launch, then `seq` (release), which the
+// host polls instead of waiting on a stream event.
+struct Snap {
+    unsigned long long best;
+    uint32_t stop;
+    uint32_t seq;  // launch sequence number + 1 (0 = never written)
 };
 
 // One launch window.  Passed by value as the kernel argument (kernarg segment,
@@ -76,12 +86,14 @@ struct Launch {
     uint32_t base_tb;      // uint8(worker_byte << rbits)
     uint32_t dmask;        // mask on the final D word for min(ntz, 8) trailing nibbles
     uint32_t ntz;          // requested trailing zeros (full digest check when > 8)
-    uint32_t done_target;  // watcher exits when Ctrl::done reaches this
+    uint32_t done_target;  // Ctrl::done once this launch's worker workgroups have retired
     uint32_t chunk;        // wave-blocks per claim
     uint64_t n_chunks;     // claims covering n_wblocks
     unsigned long long *claim;  // this launch's claim counter (zeroed before the launch)
     Ctrl *ctrl;
     const uint32_t *cancel;  // device-visible alias of the pinned host cancel flag
+    Snap *snap;              // device alias of this launch's pinned completion record
+    uint32_t seq;            // value the last workgroup writes to snap->seq
 };
 
 // Nibble positions (bit offsets) of a digest word in hex-string order from the

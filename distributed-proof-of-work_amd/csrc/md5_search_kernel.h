@@ -19,7 +19,9 @@
 //
 // Workgroup 0 of the grid is a watcher: one lane polls the pinned host
 // cancel flag (Found/Cancel, worker.go:194,209) and raises Ctrl::stop, which
-// every worker wave reads once per wave-block together with Ctrl::best.
+// every worker wave reads once per chunk together with Ctrl::best; when the
+// last worker wave retires it writes the launch's completion record (Snap)
+// to pinned host memory, which the host polls.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -37,6 +39,9 @@ namespace dpow {
 #endif
 #ifndef DPOW_ADD_MODE
 #define DPOW_ADD_MODE 0  // 0: compiler's choice (v_add3_u32); 1: two VOP2 v_add_u32
+#endif
+#ifndef DPOW_WATCH_SLEEP
+#define DPOW_WATCH_SLEEP 32  // watcher poll interval, s_sleep units of 64 cycles
 #endif
 #ifndef DPOW_NUM_SGPR
 #define DPOW_NUM_SGPR 72
@@ -141,6 +146,22 @@ DPOW_DEV bool full_check(const Launch &L, uint32_t vs, uint32_t loff) {
     return trailing_zero_nibbles(out[0][0], out[1][0], out[2][0], out[3][0]) >= L.ntz;
 }
 
+// The launch's completion record, written by the workgroup that retires last:
+// the control block after every hit of this launch (and of earlier ones) was
+// performed, then `seq` with release, which the host polls.  Out of line, and
+// not in the watcher: either inlined form makes the register allocator spill
+// SGPRs inside the hash loop (tools/isa_loop.py: 7-11 v_readlane per
+// wave-block, -3.5 % throughput).
+__device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq) {
+    const unsigned long long best = __hip_atomic_load(&ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t stop = __hip_atomic_load(&ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&snap->best, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&snap->stop, stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&snap->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Workgroup 0, one lane: relays the host cancel flag to Ctrl::stop while the
+// launch runs; exits once every worker workgroup has retired.
 DPOW_DEV void watcher(const Launch &L) {
     if (threadIdx.x != 0) return;
     for (;;) {
@@ -150,7 +171,7 @@ DPOW_DEV void watcher(const Launch &L) {
             __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        __builtin_amdgcn_s_sleep(32);
+        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
     }
 }
 
@@ -229,8 +250,12 @@ md5_search_kernel(const Launch L) {
     // Waves claim chunks of L.chunk consecutive wave-blocks from one counter, so
     // claims are handed out in increasing index order (the early exit stays
     // exact) and neither the grid size nor the residency creates a tail.  The
-    // next claim is requested while the current chunk is hashed.
-    uint64_t claim = claim_next(L.claim, lane);
+    // next claim is requested while the current chunk is hashed.  A launch that
+    // starts at or above the best index (queued behind a hit) or after a cancel
+    // claims nothing: one contended counter serves < 90 claims/us, and 8k
+    // waves' claims would hold such a launch for ~200 us.
+    const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
+    uint64_t claim = skip ? L.n_chunks : claim_next(L.claim, lane);
     while (claim < L.n_chunks) {
         const uint64_t next = claim_next(L.claim, lane);
         const uint64_t b_begin = claim * L.chunk;
@@ -253,7 +278,18 @@ md5_search_kernel(const Launch L) {
         stop = stop_next;
         claim = next;
     }
-    if (lane == 0) __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // Retirement is counted per workgroup (a quarter of the atomics on the
+    // shared counter).  Each wave's atomicMin is performed first (the
+    // workgroup-scope release waits on the wave's outstanding memory
+    // operations, with no agent-scope L2 writeback); the barrier then covers
+    // all four waves.  The workgroup whose count completes the launch
+    // publishes its completion record.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq);
+    }
 }
 
 }  // namespace dpow

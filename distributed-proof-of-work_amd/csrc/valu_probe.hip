@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "../../include/dpow_diag.h"
@@ -191,4 +193,49 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
     (void)hipEventDestroy(e1);
     (void)hipStreamDestroy(s);
     return err == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------------------
+// Launch round-trip floor of the platform (what bounds time-to-secret at small N).
+namespace {
+__global__ void ping_kernel(uint32_t *host_flag, uint32_t v) {
+    if (threadIdx.x == 0 && host_flag) __hip_atomic_store(host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+extern "C" int dpow_diag_launch_latency(int device, int mode, int reps, double *median_us) {
+    if (mode < 0 || mode > 2 || reps < 1 || !median_us) return -1;
+    if (hipSetDevice(device) != hipSuccess) return -2;
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -2;
+    uint32_t *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0) != hipSuccess)
+        return -2;
+    *h = 0;
+    std::vector<double> us;
+    int rc = 0;
+    for (int r = 0; r < reps + 5 && rc == 0; ++r) {
+        const auto t0 = std::chrono::steady_clock::now();
+        if (mode == 0) {  // launch + hipStreamSynchronize
+            hipLaunchKernelGGL(ping_kernel, dim3(1), dim3(64), 0, s, (uint32_t *)nullptr, 0u);
+            if (hipStreamSynchronize(s) != hipSuccess) rc = -2;
+        } else if (mode == 1) {  // launch + spin on a pinned word the kernel writes
+            const uint32_t v = (uint32_t)r + 1u;
+            hipLaunchKernelGGL(ping_kernel, dim3(1), dim3(64), 0, s, d, v);
+            while (__atomic_load_n(h, __ATOMIC_ACQUIRE) != v) __builtin_ia32_pause();
+        } else {  // 16-byte device->host copy + hipStreamSynchronize
+            if (hipMemcpyAsync(h + 4, d, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                rc = -2;
+        }
+        const double dt = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        if (r >= 5) us.push_back(dt);
+    }
+    (void)hipStreamSynchronize(s);
+    std::sort(us.begin(), us.end());
+    *median_us = us.empty() ? 0.0 : us[us.size() / 2];
+    (void)hipHostFree(h);
+    (void)hipStreamDestroy(s);
+    return rc;
 }

@@ -22,6 +22,13 @@ extern "C" {
  * shader clock (s_memtime / s_memrealtime).  Returns 0, or < 0 on error. */
 int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz);
 
+/* Host round trip of a one-workgroup launch on `device`, median over `reps`:
+ *   mode 0: launch + hipStreamSynchronize;
+ *   mode 1: launch + spin on a pinned host word the kernel writes (system scope);
+ *   mode 2: a 16-byte device->host hipMemcpyAsync + hipStreamSynchronize.
+ * The floor under time-to-secret at small N.  Returns 0, or < 0 on error. */
+int dpow_diag_launch_latency(int device, int mode, int reps, double *median_us);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,15 +63,18 @@ def hash_block_mix(lines):
         m = re.search(r"<[^+>]*\+0x([0-9a-f]+)>", l)
         if "branch" in mn and m:
             targets.add(base + int(m.group(1), 16))
-    best, cur = [], []
+    blocks, cur = [], []
     for a, mn, l in ins:
         if a in targets and cur:
-            best, cur = max(best, cur, key=len), []
+            blocks, cur = blocks + [cur], []
         cur.append((a, mn))
         if "branch" in mn or mn.startswith("s_endpgm"):
-            best, cur = max(best, cur, key=len), []
-    best = max(best, cur, key=len)
-    return best[0][0] - base, best[-1][0] - base, collections.Counter(mn for _, mn in best)
+            blocks, cur = blocks + [cur], []
+    blocks.append(cur)
+    # the unrolled hash: every block within 80 % of the longest (one per D-test copy)
+    longest = max(len(b) for b in blocks)
+    return [(b[0][0] - base, b[-1][0] - base, collections.Counter(mn for _, mn in b))
+            for b in blocks if len(b) >= 0.8 * longest]
 
 
 def loop_mix(lines):
@@ -113,9 +116,7 @@ def main():
     text = disasm(a.csrc, a.nblk, a.sh, a.extra)
     for w0 in [int(x) for x in a.w0.split(",")]:
         kl = kernel_lines(text, a.nblk, w0, a.sh)
-        hb = hash_block_mix(kl)
-        if hb:
-            lo, hi, c = hb
+        for lo, hi, c in hash_block_mix(kl) or []:
             valu = sum(v for k, v in c.items() if k.startswith("v_") and "lane" not in k)
             spill = c.get("v_readlane_b32", 0) + c.get("v_writelane_b32", 0)
             salu = sum(v for k, v in c.items() if k.startswith("s_"))

@@ -26,6 +26,10 @@
 #include "md5_variants.h"
 #include "plan.h"
 
+#ifndef DPOW_MAX_CHUNK
+#define DPOW_MAX_CHUNK 32
+#endif
+
 using namespace dpow;
 
 namespace {
@@ -48,17 +52,24 @@ int hip_fail(hipError_t e, const char *what) {
     } while (0)
 
 // Persistent grid: one round of resident workgroups (8 four-wave workgroups per
-// CU at <= 80 SGPRs), work handed out by in-order chunk claims.  A chunk is
-// sized for >= 16 claims per wave (small tail) and at most 32 wave-blocks
-// (one claim counter serves < 88 claims/us, MI355X_MICROARCH.md "dequeue").
+// CU at <= 80 SGPRs), work handed out by in-order chunk claims from 8 per-XCD
+// counters.  A chunk is sized for >= 16 claims per wave (small tail) and
+// within [kMinChunk, kMaxChunk] wave-blocks: a contended counter serves < 90
+// claims/us (MI355X_MICROARCH.md "dequeue") and a wave hashes one wave-block
+// in ~6 us, so 8k waves at chunk c ask ~1300/c claims/us of the 8 counters.
+// Small launches get fewer workgroups instead of smaller chunks.
 constexpr uint64_t kBlocksPerCu = 8;
 constexpr uint64_t kClaimsPerWave = 16;
-constexpr uint64_t kMaxChunk = 32;
-constexpr size_t kClaimRing = 1024;  // per-launch claim counters, zeroed per search
+constexpr uint64_t kMinChunk = 4;
+constexpr uint64_t kMaxChunk = DPOW_MAX_CHUNK;
+// Claim-counter slots (kClaimSlot counters each) used round-robin by the launches
+// of a search: zeroed at search start, re-zeroed by each launch's last workgroup.
+constexpr size_t kClaimRing = 64;
 // Launches kept in flight: launch j is queued only after the completion record
 // of launch j - kDepth shows no hit and no cancel, so a hit or a cancel leaves
 // at most kDepth launches to retire (each exits at its first check).
 constexpr size_t kDepth = 3;
+static_assert(kDepth < kClaimRing, "a claim slot is reused only after its launch completed");
 constexpr size_t kRing = 8;  // completion records and event pairs, indexed by launch seq (>= kDepth + 1)
 // Completion-record wait: spin this long (time-to-secret), then poll at kPollNs.
 constexpr int64_t kSpinNs = 200000;
@@ -79,7 +90,7 @@ struct dpow_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     Ctrl *d_ctrl = nullptr;
-    unsigned long long *d_claims = nullptr;  // kClaimRing claim counters
+    unsigned long long *d_claims = nullptr;  // kClaimRing slots of kClaimSlot claim counters
     Snap *h_snap = nullptr;        // kRing completion records: pinned, host-coherent, mapped
     Snap *d_snap = nullptr;        // device alias
     uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped
@@ -178,7 +189,7 @@ int dpow_open(int device, dpow_ctx **out) {
     c->cus = (uint32_t)prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&c->d_ctrl, sizeof(Ctrl))) != hipSuccess ||
-        (e = hipMalloc(&c->d_claims, kClaimRing * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc(&c->d_claims, kClaimRing * kClaimSlot * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_snap, kRing * sizeof(Snap), hipHostMallocCoherent | hipHostMallocMapped)) !=
             hipSuccess ||
         (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_snap), c->h_snap, 0)) != hipSuccess ||
@@ -305,7 +316,7 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     DPOW_HIP(hipSetDevice(c->device));
 
     const uint64_t bound = *best_global_idx;
-    hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)kClaimRing, bound, c->stream);
+    hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot), bound, c->stream);
     if (e != hipSuccess) return hip_fail(e, "search_reset");
 
     constexpr uint32_t wpb = kBlockThreads / 64;
@@ -347,20 +358,24 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         LaunchSlot &slot = c->slots[seq % kRing];
         if (harvest(c, slot) < 0) return DPOW_EHIP;  // the slot's previous launch
         Launch &L = pl.L;
-        unsigned long long *claim = c->d_claims + li % kClaimRing;
-        if (li >= kClaimRing) {
-            e = search_reset(nullptr, claim, 1u, 0ull, c->stream);
-            if (e != hipSuccess) return hip_fail(e, "search_reset");
-        }
         uint64_t worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
         if (worker_blocks > (uint64_t)c->cus * kBlocksPerCu) worker_blocks = (uint64_t)c->cus * kBlocksPerCu;
         uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
-        if (chunk < 1) chunk = 1;
+        if (chunk < kMinChunk) chunk = kMinChunk;
         if (chunk > kMaxChunk) chunk = kMaxChunk;
+        const uint64_t n_chunks = (L.n_wblocks + chunk - 1) / chunk;
+        // No more waves than chunks, but a worker block for every counter that
+        // holds a chunk (block b serves counter (b - 1) % kClaimCounters).
+        uint64_t need_blocks = (n_chunks + wpb - 1) / wpb;
+        if (need_blocks < n_chunks && need_blocks < kClaimCounters)
+            need_blocks = n_chunks < kClaimCounters ? n_chunks : kClaimCounters;
+        if (worker_blocks > need_blocks) worker_blocks = need_blocks;
+        if (worker_blocks < kClaimCounters && worker_blocks < n_chunks)
+            return set_error(DPOW_EINVAL, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.chunk = (uint32_t)chunk;
-        L.n_chunks = (L.n_wblocks + chunk - 1) / chunk;
-        L.claim = claim;
+        L.n_chunks = n_chunks;
+        L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;
         L.cancel = c->d_cancel;

@@ -54,6 +54,13 @@ constexpr uint32_t kBop3I = 0x39;  // I = y ^ (x | ~z)
 constexpr int kNC = DPOW_NC;
 constexpr int kWaveBlock = 64 * kNC;  // local indices per wave-block
 constexpr int kBlockThreads = 256;    // 4 waves per workgroup
+// Claim counters per launch: one per XCD (workgroup b runs on XCD b % 8), each
+// on its own 128-byte line.  Counter x hands out chunks x, x + 8, x + 16, ...
+// in increasing order, so the early exit stays exact per counter, and eight
+// counters serve eight times the claim rate of one.
+constexpr uint32_t kClaimCounters = 8;
+constexpr uint32_t kClaimStride = 16;  // unsigned long long units (128 B)
+constexpr uint32_t kClaimSlot = kClaimCounters * kClaimStride;  // one launch's counters
 
 // Device control block (one per context, in HBM).
 struct Ctrl {
@@ -89,7 +96,8 @@ struct Launch {
     uint32_t done_target;  // Ctrl::done once this launch's worker workgroups have retired
     uint32_t chunk;        // wave-blocks per claim
     uint64_t n_chunks;     // claims covering n_wblocks
-    unsigned long long *claim;  // this launch's claim counter (zeroed before the launch)
+    unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
+                                //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;
     const uint32_t *cancel;  // device-visible alias of the pinned host cancel flag
     Snap *snap;              // device alias of this launch's pinned completion record

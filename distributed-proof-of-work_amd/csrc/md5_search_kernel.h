@@ -43,6 +43,9 @@ namespace dpow {
 #ifndef DPOW_WATCH_SLEEP
 #define DPOW_WATCH_SLEEP 32  // watcher poll interval, s_sleep units of 64 cycles
 #endif
+#ifndef DPOW_STEAL
+#define DPOW_STEAL 1  // a wave whose counter drained claims from the next counter (A/B switch)
+#endif
 #ifndef DPOW_NUM_SGPR
 #define DPOW_NUM_SGPR 72
 #endif
@@ -152,7 +155,9 @@ DPOW_DEV bool full_check(const Launch &L, uint32_t vs, uint32_t loff) {
 // not in the watcher: either inlined form makes the register allocator spill
 // SGPRs inside the hash loop (tools/isa_loop.py: 7-11 v_readlane per
 // wave-block, -3.5 % throughput).
-__device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq) {
+__device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim) {
+    // Every workgroup has left its claim loop: recycle the counter slot.
+    for (uint32_t x = 0; x < kClaimCounters; ++x) claim[x * kClaimStride] = 0ull;
     const unsigned long long best = __hip_atomic_load(&ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t stop = __hip_atomic_load(&ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&snap->best, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -175,13 +180,14 @@ DPOW_DEV void watcher(const Launch &L) {
     }
 }
 
-// One returning atomic per claim, by lane 0, broadcast to the wave.
-DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t lane) {
+// One returning atomic per claim, by lane 0, broadcast to the wave; the
+// counter's n-th claim is chunk n * kClaimCounters + x.
+DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t x, uint32_t lane) {
     unsigned long long v = 0;
     if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
+    return (((uint64_t)hi << 32) | lo) * kClaimCounters + x;
 }
 
 DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
@@ -247,17 +253,38 @@ md5_search_kernel(const Launch L) {
     unsigned long long best = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t stop = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-    // Waves claim chunks of L.chunk consecutive wave-blocks from one counter, so
-    // claims are handed out in increasing index order (the early exit stays
-    // exact) and neither the grid size nor the residency creates a tail.  The
-    // next claim is requested while the current chunk is hashed.  A launch that
-    // starts at or above the best index (queued behind a hit) or after a cancel
-    // claims nothing: one contended counter serves < 90 claims/us, and 8k
-    // waves' claims would hold such a launch for ~200 us.
+    // Waves claim chunks of L.chunk consecutive wave-blocks from their XCD's
+    // counter, which hands its chunks out in increasing index order (the early
+    // exit stays exact); neither the grid size nor the residency creates a
+    // tail.  The next claim is requested while the current chunk is hashed.  A
+    // launch that starts at or above the best index (queued behind a hit) or
+    // after a cancel claims nothing: a contended counter serves < 90 claims/us.
+    // Worker block b (>= 1) serves counter (b - 1) % 8; the host launches at
+    // least min(n_chunks, 8) worker blocks, so every counter holding a chunk
+    // has waves.  Workgroups go round-robin to XCDs, so each counter's waves
+    // share one XCD.
+    uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
-    uint64_t claim = skip ? L.n_chunks : claim_next(L.claim, lane);
-    while (claim < L.n_chunks) {
-        const uint64_t next = claim_next(L.claim, lane);
+    uint64_t claim = skip ? L.n_chunks : claim_next(L.claim + x * kClaimStride, x, lane);
+    uint32_t hops = 0;
+    for (;;) {
+#if DPOW_STEAL
+        // This counter is drained: move on to the next one (its waves may sit
+        // on a slower XCD).  A counter only ever drains, so after a full round
+        // of drained counters every chunk has been handed out.
+        if (claim >= L.n_chunks) {
+            if (skip || ++hops >= kClaimCounters) break;
+            x = (x + 1u) % kClaimCounters;
+            const unsigned long long seen =
+                __hip_atomic_load(L.claim + x * kClaimStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            claim = seen * kClaimCounters + x < L.n_chunks ? claim_next(L.claim + x * kClaimStride, x, lane)
+                                                             : L.n_chunks;
+            continue;
+        }
+#else
+        if (claim >= L.n_chunks) break;
+#endif
+        const uint64_t next = claim_next(L.claim + x * kClaimStride, x, lane);
         const uint64_t b_begin = claim * L.chunk;
         const uint32_t nb = (uint32_t)(b_begin + L.chunk < L.n_wblocks ? L.chunk : L.n_wblocks - b_begin);
         const uint64_t i_first = L.wb_begin + b_begin * (uint64_t)kWaveBlock;
@@ -288,7 +315,7 @@ md5_search_kernel(const Launch L) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq);
+        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim);
     }
 }
 

@@ -200,3 +200,59 @@ def test_native_cli(tmp_path):
     out = json.loads(subprocess.check_output([cli, "sweep", "32"], timeout=120).decode())
     assert out["status"] == 0 and out["candidates"] == 1 << 32
     print("cli sweep", out)
+
+
+def test_claim_slot_recycling_many_launches(miner, oracle):
+    """A window of 80 launches (worker_bits = 8: one thread byte per k, so each
+    2^24-k launch of the L = 4 segment holds 2^24 candidates) recycles the 64
+    claim-counter slots: the whole window is hashed exactly once."""
+    k0 = 1 << 24
+    k1 = k0 + 80 * (1 << 24)
+    miner.reset_stats()
+    assert miner.search([1, 2, 3, 4], 32, 77, 8, k0, k1).status == EXHAUSTED
+    s = miner.stats()
+    assert s.launches == 80 and s.candidates == 80 * (1 << 24)
+    # A late first hit in the same partition: hashlib-valid, and the oracle
+    # agrees on the 4097 candidates ending at it (no earlier hit there).
+    r = miner.search([1, 2, 3, 4], 8, 77, 8, k0, k1 + 400 * (1 << 24))
+    assert r.status == FOUND and _hexz([1, 2, 3, 4], r.secret).endswith("0" * 8)
+    k_hit = r.global_idx >> 8
+    exp = oracle.mine_window([1, 2, 3, 4], 8, 77, 8, max(k0, k_hit - 4096), k_hit + 1)
+    assert exp is not None and (exp[0], exp[1]) == (list(r.secret), r.global_idx)
+    # The same window cut just below the hit: nothing before it, the same hit after.
+    assert miner.search([1, 2, 3, 4], 8, 77, 8, k0, k_hit).status == EXHAUSTED
+    r2 = miner.search([1, 2, 3, 4], 8, 77, 8, k_hit, k1 + 400 * (1 << 24))
+    assert r2.status == FOUND and r2.global_idx == r.global_idx
+
+
+def test_back_to_back_after_early_returns(miner, golden):
+    """A search that returns at a hit leaves up to 3 queued launches behind it
+    (they claim nothing); the next searches on the context must not see them."""
+    e5 = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 5)
+    for _ in range(20):
+        r = miner.search([1, 2, 3, 4], 3, 0, 0, 0, 1 << 26)
+        assert r.status == FOUND and r.global_idx == 97
+        miner.reset_stats()
+        assert miner.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + 4096).status == EXHAUSTED
+        s = miner.stats()
+        assert s.launches == 1 and s.candidates == 4096 * 256
+        r = miner.search([1, 2, 3, 4], 5, 0, 0, 0, 1 << 26)
+        assert r.status == FOUND and r.global_idx == e5["global_idx"]
+
+
+def test_small_launch_grids_vs_oracle(miner, oracle):
+    """Launches of 1..40 k per partition: grids of a few workgroups, fewer than
+    the 8 claim counters, chunks of the minimum size."""
+    rnd = random.Random(8)
+    for wbits in (0, 3, 6, 8):
+        wb = rnd.randrange(1 << wbits) if wbits else 0
+        for n in list(range(1, 18)) + [24, 33, 40]:
+            k0 = rnd.choice([0, 1, 200, 300, 70000, (1 << 24) + 5])
+            ntz = rnd.choice([1, 2, 3])
+            exp = oracle.mine_window([7, 7, 7, 7], ntz, wb, wbits, k0, k0 + n)
+            r = miner.search([7, 7, 7, 7], ntz, wb, wbits, k0, k0 + n)
+            if exp is None:
+                assert r.status == EXHAUSTED, (wbits, wb, k0, n, ntz)
+            else:
+                assert r.status == FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1]), \
+                    (wbits, wb, k0, n, ntz, r, exp)

@@ -37,9 +37,6 @@ namespace dpow {
 #ifndef DPOW_FOLD_ZERO
 #define DPOW_FOLD_ZERO 1  // fold always-zero message words to literal K (A/B switch)
 #endif
-#ifndef DPOW_ADD_MODE
-#define DPOW_ADD_MODE 0  // 0: compiler's choice (v_add3_u32); 1: two VOP2 v_add_u32
-#endif
 #ifndef DPOW_WATCH_SLEEP
 #define DPOW_WATCH_SLEEP 32  // watcher poll interval, s_sleep units of 64 cycles
 #endif
@@ -64,65 +61,243 @@ struct VarWords {
     uint32_t hi[kNC];    // V >> (32 - 8*SH), added for steps reading word W0+1
 };
 
-template <int NBLK, int W0, int SH, int BLK, int I, int NCAND>
+// K + M of step I of block BLK for candidate j (the message word M includes the
+// candidate's variable bytes when the step reads word W0, or W0 + 1 for SH != 0).
+template <int NBLK, int W0, int SH, int BLK, int I>
+struct StepWord {
+    static constexpr int m = 16 * BLK + md5_word(I);
+    // Words past the variable bytes, the chunk tail and the 0x80 pad -- every
+    // word after W0 + 2 except the bit-length word -- are zero for every launch
+    // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
+    static constexpr bool zero_word = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
+    static constexpr bool per_lane = m == W0 || (SH != 0 && m == W0 + 1);
+    static DPOW_DEV uint32_t km(const Launch &L, const VarWords &v, int j) {
+        uint32_t k = zero_word ? kMd5K[I] : L.KT[64 * BLK + I];
+        if constexpr (m == W0) k = (k + v.lo_s[j]) + v.lo_v;
+        if constexpr (SH != 0 && m == W0 + 1) k += v.hi[j];
+        return k;
+    }
+};
+
+// Steps [I, IE) of block BLK for NCAND candidates, left to the compiler.
+template <int NBLK, int W0, int SH, int BLK, int I, int IE, int NCAND>
 DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
-    if constexpr (I < 64) {
+    if constexpr (I < IE) {
         constexpr int ai = (64 - I) % 4, bi = (ai + 1) % 4, ci = (ai + 2) % 4, di = (ai + 3) % 4;
-        constexpr int m = 16 * BLK + md5_word(I);
         constexpr int s = md5_shift(I);
-        // Words past the variable bytes, the chunk tail and the 0x80 pad -- every
-        // word after W0 + 2 except the bit-length word -- are zero for every launch
-        // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
-        constexpr bool zero_word = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
-        const uint32_t kt = zero_word ? kMd5K[I] : L.KT[64 * BLK + I];
 #pragma unroll
         for (int j = 0; j < NCAND; ++j) {
-            uint32_t km = kt;
-            if constexpr (m == W0) km = (km + v.lo_s[j]) + v.lo_v;
-            if constexpr (SH != 0 && m == W0 + 1) km += v.hi[j];
+            const uint32_t km = StepWord<NBLK, W0, SH, BLK, I>::km(L, v, j);
             const uint32_t f = md5_fn<I>(x[bi][j], x[ci][j], x[di][j]);
-#if DPOW_ADD_MODE == 1
-            // a + f + km as two full-rate VOP2 adds (K as an inline literal when the word is zero)
-            if constexpr (BLK > 0 || I > W0 + 1) {
-                uint32_t t;
-                if constexpr (zero_word)
-                    asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "i"(kMd5K[I]), "v"(x[ai][j]));
-                else if constexpr (m == W0 || (SH != 0 && m == W0 + 1))
-                    asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "v"(km), "v"(x[ai][j]));
-                else
-                    asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "s"(km), "v"(x[ai][j]));
-                asm("v_add_u32_e32 %0, %1, %2" : "=v"(t) : "v"(f), "v"(t));
-                x[ai][j] = x[bi][j] + __builtin_rotateleft32(t, s);
-            } else {
-                x[ai][j] = x[bi][j] + __builtin_rotateleft32(x[ai][j] + f + km, s);
-            }
-#else
             x[ai][j] = x[bi][j] + __builtin_rotateleft32(x[ai][j] + f + km, s);
-#endif
         }
-        md5_steps<NBLK, W0, SH, BLK, I + 1, NCAND>(x, L, v);
+        md5_steps<NBLK, W0, SH, BLK, I + 1, IE, NCAND>(x, L, v);
     }
 }
 
+// ---------------------------------------------------------------------------
+// Two candidates, issue order fixed by hand.  Each MD5 step is four VALU
+// instructions, two full rate (v_bitop3_b32, v_add_u32) and two half rate
+// (v_add3_u32, v_alignbit_b32).  gfx950 issues this mix ~6 % faster when full-
+// and half-rate instructions strictly alternate than in the compiler's order
+// (dpow_diag_valu_rate kinds 5/20/22: 44.1 / 43.0 / 46.9 T lane-op/s), so
+// candidate q runs half a step behind candidate p and each step pair issues
+//   F bop p(I) | H rot q(I-1) | F add q(I-1) | H add3 p(I) | F bop q(I) | H rot p(I) | F add p(I) | H add3 q(I)
+// One asm statement per step pair: the compiler keeps the order, allocates the
+// registers and places the SALU moves of the K constants, and inserts no
+// hazard padding inside the group (these plain VALU ops are interlocked in
+// hardware; per-instruction asm statements got an s_nop after every VOP3).
+namespace pipe {
+
+template <int I>
+constexpr uint32_t tt() {
+    return I / 16 == 0 ? kBop3F : I / 16 == 1 ? kBop3G : I / 16 == 2 ? kBop3H : kBop3I;
+}
+
+template <int I> struct Roles {
+    static constexpr int a = (64 - I) % 4, b = (a + 1) % 4, c = (a + 2) % 4, d = (a + 3) % 4;
+};
+
+// Wait states after each instruction kind of a group (-1: none).  A VALU
+// instruction issued right behind the one it depends on holds the SIMD's issue
+// for the whole dependency latency -- every wave on the SIMD waits -- while an
+// s_nop holds only its own wave and lets the other waves issue.  Measured on
+// the sweep (profiles/r01_ab_nop.log): no padding 170 GH/s; s_nop 0 after each
+// rotate (its add depends on it) 192.5; plus s_nop 0 / 1 / 2 / 3 after each
+// add3 200.7 / 203.6 / 209.1 / 205.4; s_nop 1 after the rotate instead 191;
+// any padding after the full-rate ops 168-185; no rotate padding 179-180.
+#ifndef DPOW_NOP_B
+#define DPOW_NOP_B -1  // after v_bitop3_b32
+#endif
+#ifndef DPOW_NOP_R
+#define DPOW_NOP_R 0  // after v_alignbit_b32 (the rotate; the next add reads it)
+#endif
+#ifndef DPOW_NOP_D
+#define DPOW_NOP_D -1  // after v_add_u32
+#endif
+#ifndef DPOW_NOP_A
+#define DPOW_NOP_A 2  // after v_add3_u32
+#endif
+#define DPOW_STR2(x) #x
+#define DPOW_STR(x) DPOW_STR2(x)
+#if DPOW_NOP_B >= 0
+#define DPOW_PAD_B "s_nop " DPOW_STR(DPOW_NOP_B) "\n\t"
+#else
+#define DPOW_PAD_B ""
+#endif
+#if DPOW_NOP_R >= 0
+#define DPOW_PAD_R "s_nop " DPOW_STR(DPOW_NOP_R) "\n\t"
+#else
+#define DPOW_PAD_R ""
+#endif
+#if DPOW_NOP_D >= 0
+#define DPOW_PAD_D "s_nop " DPOW_STR(DPOW_NOP_D) "\n\t"
+#else
+#define DPOW_PAD_D ""
+#endif
+#if DPOW_NOP_A >= 0
+#define DPOW_PAD_A "s_nop " DPOW_STR(DPOW_NOP_A) "\n\t"
+#else
+#define DPOW_PAD_A ""
+#endif
+
+#define DPOW_PIPE_BODY                                                     \
+    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \
+    "v_alignbit_b32 %[rq], %[tq], %[tq], %[sq]\n\t" DPOW_PAD_R            \
+    "v_add_u32_e32 %[qb], %[qc], %[rq]\n\t" DPOW_PAD_D                    \
+    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A                \
+    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" DPOW_PAD_B \
+    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R            \
+    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t" DPOW_PAD_D                    \
+    "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
+
+#define DPOW_PIPE_PRO                                                      \
+    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \
+    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A                \
+    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" DPOW_PAD_B \
+    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R            \
+    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t" DPOW_PAD_D                    \
+    "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
+
+// One step pair of candidates p = J, q = J + 1 at step I (q finishes step I-1,
+// whose add3 is in tq, and starts step I).
+template <int NBLK, int W0, int SH, int BLK, int I, int J>
+DPOW_DEV void body(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const VarWords &v) {
+    using R = Roles<I>;  // q's step I-1 writes x[R::b][q] from x[R::c][q]
+    using W = StepWord<NBLK, W0, SH, BLK, I>;
+    const uint32_t kp = W::km(L, v, J), kq = W::km(L, v, J + 1);
+    uint32_t fp, fq, rq, tp;
+    if constexpr (W::per_lane)
+        asm volatile(DPOW_PIPE_BODY
+                     : [pa] "+v"(x[R::a][J]), [qb] "=&v"(x[R::b][J + 1]), [tq] "+v"(tq), [fp] "=&v"(fp),
+                       [fq] "=&v"(fq), [rq] "=&v"(rq), [tp] "=&v"(tp)
+                     : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qc] "v"(x[R::c][J + 1]),
+                       [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "v"(kp), [kq] "v"(kq),
+                       [tt] "i"(tt<I>()), [sp] "i"(32 - md5_shift(I)), [sq] "i"(32 - md5_shift(I - 1)));
+    else
+        asm volatile(DPOW_PIPE_BODY
+                     : [pa] "+v"(x[R::a][J]), [qb] "=&v"(x[R::b][J + 1]), [tq] "+v"(tq), [fp] "=&v"(fp),
+                       [fq] "=&v"(fq), [rq] "=&v"(rq), [tp] "=&v"(tp)
+                     : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qc] "v"(x[R::c][J + 1]),
+                       [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "s"(kp), [kq] "s"(kq),
+                       [tt] "i"(tt<I>()), [sp] "i"(32 - md5_shift(I)), [sq] "i"(32 - md5_shift(I - 1)));
+}
+
+// Prologue of a pair at its first pipelined step I0: q's step I0 is left half done.
+template <int NBLK, int W0, int SH, int BLK, int I0, int J>
+DPOW_DEV void prologue(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const VarWords &v) {
+    using R = Roles<I0>;
+    using W = StepWord<NBLK, W0, SH, BLK, I0>;
+    const uint32_t kp = W::km(L, v, J), kq = W::km(L, v, J + 1);
+    uint32_t fp, fq, tp;
+    if constexpr (W::per_lane)
+        asm volatile(DPOW_PIPE_PRO
+                     : [pa] "+v"(x[R::a][J]), [tq] "=&v"(tq), [fp] "=&v"(fp), [fq] "=&v"(fq), [tp] "=&v"(tp)
+                     : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qb] "v"(x[R::b][J + 1]),
+                       [qc] "v"(x[R::c][J + 1]), [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "v"(kp),
+                       [kq] "v"(kq), [tt] "i"(tt<I0>()), [sp] "i"(32 - md5_shift(I0)));
+    else
+        asm volatile(DPOW_PIPE_PRO
+                     : [pa] "+v"(x[R::a][J]), [tq] "=&v"(tq), [fp] "=&v"(fp), [fq] "=&v"(fq), [tp] "=&v"(tp)
+                     : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qb] "v"(x[R::b][J + 1]),
+                       [qc] "v"(x[R::c][J + 1]), [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "s"(kp),
+                       [kq] "s"(kq), [tt] "i"(tt<I0>()), [sp] "i"(32 - md5_shift(I0)));
+}
+
+constexpr int kPairs = kNC / 2;
+
+// Step pairs I .. IE-1 of every candidate pair, the pairs' groups interleaved.
+template <int NBLK, int W0, int SH, int BLK, int I, int IE>
+DPOW_DEV void run(uint32_t (&x)[4][kNC], uint32_t (&tq)[kPairs], const Launch &L, const VarWords &v) {
+    if constexpr (I < IE) {
+        body<NBLK, W0, SH, BLK, I, 0>(x, tq[0], L, v);
+        if constexpr (kPairs > 1) body<NBLK, W0, SH, BLK, I, 2>(x, tq[1], L, v);
+        run<NBLK, W0, SH, BLK, I + 1, IE>(x, tq, L, v);
+    }
+}
+
+// Steps [I0, IE) of block BLK for all candidates in the alternating order.
+template <int NBLK, int W0, int SH, int BLK, int I0, int IE>
+DPOW_DEV void steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
+    static_assert(kNC == 2 || kNC == 4, "the pipelined path runs one or two candidate pairs");
+    if constexpr (I0 < IE) {
+        uint32_t tq[kPairs];
+        prologue<NBLK, W0, SH, BLK, I0, 0>(x, tq[0], L, v);
+        if constexpr (kPairs > 1) prologue<NBLK, W0, SH, BLK, I0, 2>(x, tq[1], L, v);
+        run<NBLK, W0, SH, BLK, I0 + 1, IE>(x, tq, L, v);
+        // epilogue: each q finishes step IE-1
+        using E = Roles<IE - 1>;
+#pragma unroll
+        for (int p = 0; p < kPairs; ++p)
+            x[E::a][2 * p + 1] = x[E::b][2 * p + 1] + __builtin_rotateleft32(tq[p], md5_shift(IE - 1));
+    }
+}
+
+#undef DPOW_PIPE_BODY
+#undef DPOW_PIPE_PRO
+#undef DPOW_PAD_B
+#undef DPOW_PAD_R
+#undef DPOW_PAD_D
+#undef DPOW_PAD_A
+
+}  // namespace pipe
+
+#ifndef DPOW_PIPE
+#define DPOW_PIPE 1  // hand-ordered alternating issue for the two-candidate hash (A/B switch)
+#endif
+
 // Final-block compression(s) of NCAND candidates; returns the digest words.
-template <int NBLK, int W0, int SH, int NCAND>
+// With ONLY_D the last block stops after step 61, which writes D (steps 62-63
+// only feed A..C): out[3] is exact, out[0..2] are not computed.
+template <int NBLK, int W0, int SH, int NCAND, bool ONLY_D = false>
 DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords &v) {
     uint32_t x[4][kNC];
 #pragma unroll
     for (int j = 0; j < NCAND; ++j) {
         x[0][j] = L.iv[0]; x[1][j] = L.iv[1]; x[2][j] = L.iv[2]; x[3][j] = L.iv[3];
     }
-    md5_steps<NBLK, W0, SH, 0, 0, NCAND>(x, L, v);
+    // The pipelined order needs all four state words per lane: from step W0 + 4
+    // of the first block on (earlier steps are wave-uniform or partly so, and
+    // the compiler folds them).
+    constexpr bool kPipe = DPOW_PIPE && NCAND == kNC && (kNC == 2 || kNC == 4);
+    constexpr int kEnd0 = (ONLY_D && NBLK == 1) ? 62 : 64;
+    constexpr int kI0 = kPipe ? (W0 + 4 < kEnd0 ? W0 + 4 : kEnd0) : kEnd0;
+    md5_steps<NBLK, W0, SH, 0, 0, kI0, NCAND>(x, L, v);
+    if constexpr (kPipe) pipe::steps<NBLK, W0, SH, 0, kI0, kEnd0>(x, L, v);
 #pragma unroll
     for (int j = 0; j < NCAND; ++j)
 #pragma unroll
         for (int w = 0; w < 4; ++w) out[w][j] = L.iv[w] + x[w][j];
     if constexpr (NBLK == 2) {
+        constexpr int kEnd1 = ONLY_D ? 62 : 64;
 #pragma unroll
         for (int j = 0; j < NCAND; ++j)
 #pragma unroll
             for (int w = 0; w < 4; ++w) x[w][j] = out[w][j];
-        md5_steps<NBLK, W0, SH, 1, 0, NCAND>(x, L, v);
+        if constexpr (kPipe)
+            pipe::steps<NBLK, W0, SH, 1, 0, kEnd1>(x, L, v);
+        else
+            md5_steps<NBLK, W0, SH, 1, 0, kEnd1, NCAND>(x, L, v);
 #pragma unroll
         for (int j = 0; j < NCAND; ++j)
 #pragma unroll
@@ -212,7 +387,7 @@ DPOW_DEV unsigned long long hash_wave_block(const Launch &L, uint64_t i0, uint32
         var_words<SH>(v, j, vs[j], loff);
     }
     uint32_t dig[4][kNC];
-    md5_tail<NBLK, W0, SH, kNC>(dig, L, v);
+    md5_tail<NBLK, W0, SH, kNC, true>(dig, L, v);  // only D is tested here
 
     uint64_t bal[kNC];
     uint64_t any = 0;

@@ -48,6 +48,8 @@ __global__ void __launch_bounds__(kThreads) valu_probe_kernel(uint32_t *out, uin
     const uint32_t c = blockIdx.x + 0x7F4A7C15u + threadIdx.x;
 #pragma unroll
     for (int j = 0; j < kChains; ++j) x[j] = threadIdx.x + 17u * j;
+    const uint32_t ks = __builtin_amdgcn_readfirstlane(c);
+    uint32_t tqv = x[5] ^ ks;  // kind 25: q's pending half step
     uint64_t t0 = 0, r0 = 0;
     if (threadIdx.x == 0) {
         t0 = __builtin_amdgcn_s_memtime();
@@ -91,6 +93,88 @@ __global__ void __launch_bounds__(kThreads) valu_probe_kernel(uint32_t *out, uin
 #pragma unroll
                         for (int q = 0; q < 2; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j + q]) : "v"(b));
                     }
+                } else if constexpr (KIND == 22) {
+                    // two chains software-pipelined so full- and half-rate instructions
+                    // alternate: F(p) H(q) F(q) H(p) F(q) H(p) F(p) H(q)
+                    if (j % 2 == 0) {
+                        uint32_t &p = x[j], &q = x[j + 1];
+                        uint32_t fp, fq;
+                        asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(fp) : "v"(p), "v"(b), "v"(c));
+                        asm volatile("v_alignbit_b32 %0, %0, %0, 25" : "+v"(q));
+                        asm volatile("v_add_u32 %0, %0, %1" : "+v"(q) : "v"(b));
+                        asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(p) : "v"(fp), "v"(c));
+                        asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(fq) : "v"(q), "v"(b), "v"(c));
+                        asm volatile("v_alignbit_b32 %0, %0, %0, 25" : "+v"(p));
+                        asm volatile("v_add_u32 %0, %0, %1" : "+v"(p) : "v"(b));
+                        asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(q) : "v"(fq), "v"(c));
+                    }
+                } else if constexpr (KIND == 24) {
+                    // real MD5 dependency structure: 2 candidates x 4 state words
+                    // (x[0..3], x[4..7]), step I = 4 u + j / 2, compiler-ordered
+                    if (j % 2 == 0) {
+                        const int I = 4 * u + j / 2;
+                        const int a = (64 - I) % 4, bb = (a + 1) % 4, cc = (a + 2) % 4, d = (a + 3) % 4;
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            uint32_t *y = x + 4 * q;
+                            const uint32_t f = __builtin_amdgcn_bitop3_b32(y[bb], y[cc], y[d], 0xCA);
+                            y[a] = y[bb] + __builtin_rotateleft32(y[a] + f + ks, 7 + (I % 4) * 5);
+                        }
+                    }
+                } else if constexpr (KIND == 25) {
+                    // the same in the search kernel's hand-ordered alternating groups
+                    if (j % 2 == 0) {
+                        const int I = 4 * u + j / 2;
+                        const int a = (64 - I) % 4, bb = (a + 1) % 4, cc = (a + 2) % 4, d = (a + 3) % 4;
+                        uint32_t fp, fq, rq, tp;
+                        asm volatile(
+                            "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:0xca\n\t"
+                            "v_alignbit_b32 %[rq], %[tq], %[tq], 25\n\t"
+                            "v_add_u32_e32 %[qb], %[qc], %[rq]\n\t"
+                            "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t"
+                            "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:0xca\n\t"
+                            "v_alignbit_b32 %[tp], %[tp], %[tp], 25\n\t"
+                            "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t"
+                            "v_add3_u32 %[tq], %[qa], %[fq], %[kq]"
+                            : [pa] "+v"(x[a]), [qb] "=&v"(x[4 + bb]), [tq] "+v"(tqv), [fp] "=&v"(fp), [fq] "=&v"(fq),
+                              [rq] "=&v"(rq), [tp] "=&v"(tp)
+                            : [pb] "v"(x[bb]), [pc] "v"(x[cc]), [pd] "v"(x[d]), [qc] "v"(x[4 + cc]), [qd] "v"(x[4 + d]),
+                              [qa] "v"(x[4 + a]), [kp] "s"(ks), [kq] "s"(ks));
+                    }
+                } else if constexpr (KIND == 26 || KIND == 27) {
+                    // kind 22's alternating pairs on fixed registers (4 pairs p/q = v24+4k / v25+4k):
+                    // 26 reads operands from distinct VGPR banks (index mod 4), 27 from one bank
+                    if (j % 2 == 0) {
+#define DPOW_PAIR(P, Q, B, C, FP, FQ)                                                          \
+    "v_bitop3_b32 " FP ", " P ", " B ", " C " bitop3:0xca\n\t"                                 \
+    "v_alignbit_b32 " Q ", " Q ", " Q ", 25\n\t"                                               \
+    "v_add_u32_e32 " Q ", " Q ", " B "\n\t"                                                    \
+    "v_add3_u32 " P ", " P ", " FP ", " C "\n\t"                                              \
+    "v_bitop3_b32 " FQ ", " Q ", " B ", " C " bitop3:0xca\n\t"                                 \
+    "v_alignbit_b32 " P ", " P ", " P ", 25\n\t"                                               \
+    "v_add_u32_e32 " P ", " P ", " B "\n\t"                                                    \
+    "v_add3_u32 " Q ", " Q ", " FQ ", " C "\n\t"
+                        if constexpr (KIND == 26) {
+                            if (j == 0) asm volatile(DPOW_PAIR("v24", "v25", "v14", "v19", "v41", "v40") ::: "v24", "v25", "v40", "v41");
+                            if (j == 2) asm volatile(DPOW_PAIR("v28", "v29", "v14", "v19", "v41", "v40") ::: "v28", "v29", "v40", "v41");
+                            if (j == 4) asm volatile(DPOW_PAIR("v32", "v33", "v14", "v19", "v41", "v40") ::: "v32", "v33", "v40", "v41");
+                            if (j == 6) asm volatile(DPOW_PAIR("v36", "v37", "v14", "v19", "v41", "v40") ::: "v36", "v37", "v40", "v41");
+                        } else {
+                            if (j == 0) asm volatile(DPOW_PAIR("v24", "v25", "v12", "v16", "v40", "v41") ::: "v24", "v25", "v40", "v41");
+                            if (j == 2) asm volatile(DPOW_PAIR("v28", "v29", "v12", "v16", "v40", "v41") ::: "v28", "v29", "v40", "v41");
+                            if (j == 4) asm volatile(DPOW_PAIR("v32", "v33", "v12", "v16", "v40", "v41") ::: "v32", "v33", "v40", "v41");
+                            if (j == 6) asm volatile(DPOW_PAIR("v36", "v37", "v12", "v16", "v40", "v41") ::: "v36", "v37", "v40", "v41");
+                        }
+#undef DPOW_PAIR
+                    }
+                } else if constexpr (KIND == 23) {
+                    // MD5 step mix with the K operand from an SGPR (as in the kernel)
+                    uint32_t f;
+                    const uint32_t k = __builtin_amdgcn_readfirstlane(c);
+                    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(f) : "v"(x[j]), "v"(b), "v"(c));
+                    asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[j]) : "v"(f), "s"(k));
+                    asm volatile("v_alignbit_b32 %0, %0, %0, 25" : "+v"(x[j]));
+                    asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j]) : "v"(b));
                 } else if constexpr (KIND == 5) {
                     uint32_t f = x[j];
                     asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(f) : "v"(x[j]), "v"(b), "v"(c));
@@ -109,7 +193,7 @@ __global__ void __launch_bounds__(kThreads) valu_probe_kernel(uint32_t *out, uin
         clk[2 * blockIdx.x] = t1 - t0;
         clk[2 * blockIdx.x + 1] = r1 - r0;
     }
-    uint32_t acc = 0;
+    uint32_t acc = tqv;
 #pragma unroll
     for (int j = 0; j < kChains; ++j) acc ^= x[j];
     out[blockIdx.x * kThreads + threadIdx.x] = acc;
@@ -124,7 +208,7 @@ hipError_t run(uint32_t blocks, uint32_t iters, uint32_t *out, uint64_t *clk, hi
 }  // namespace
 
 extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz) {
-    if (kind < 0 || kind > 21 || !lane_ops_per_s || !clock_ghz) return -1;
+    if (kind < 0 || kind > 27 || !lane_ops_per_s || !clock_ghz) return -1;
     if (hipSetDevice(device) != hipSuccess) return -2;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -2;
@@ -162,7 +246,13 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             case 18: return run<18>(blocks, iters, out, clk, s);
             case 19: return run<19>(blocks, iters, out, clk, s);
             case 20: return run<20>(blocks, iters, out, clk, s);
-            default: return run<21>(blocks, iters, out, clk, s);
+            case 21: return run<21>(blocks, iters, out, clk, s);
+            case 22: return run<22>(blocks, iters, out, clk, s);
+            case 23: return run<23>(blocks, iters, out, clk, s);
+            case 24: return run<24>(blocks, iters, out, clk, s);
+            case 25: return run<25>(blocks, iters, out, clk, s);
+            case 26: return run<26>(blocks, iters, out, clk, s);
+            default: return run<27>(blocks, iters, out, clk, s);
         }
     };
     hipError_t err = hipSuccess;
@@ -184,7 +274,7 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             ++n;
         }
     const double instr_per_lane =
-        (double)iters * kUnroll * kChains * (kind == 5 || kind == 19 || kind == 20 ? 4 : kind == 21 ? 5 : 1);
+        (double)iters * kUnroll * kChains * (kind == 5 || kind == 19 || kind == 20 || kind >= 22 ? 4 : kind == 21 ? 5 : 1);
     *lane_ops_per_s = instr_per_lane * (double)blocks * kThreads * reps / (ms * 1e-3);
     *clock_ghz = n ? ratio / n * 0.1 : 0.0;  // s_memrealtime ticks at 100 MHz
     (void)hipFree(out);

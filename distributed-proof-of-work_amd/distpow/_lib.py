@@ -124,7 +124,10 @@ VALU_KINDS = {0: "v_add_u32", 1: "v_add3_u32", 2: "v_alignbit_b32", 3: "v_bitop3
               5: "md5_step_mix", 6: "v_lshl_add_u32", 7: "v_lshl_or_b32", 8: "v_xad_u32", 9: "v_perm_b32",
               10: "v_lshlrev_b32", 11: "v_or3_b32", 12: "v_add_u32_literal", 13: "v_alignbyte_b32",
               14: "v_bfi_b32", 15: "v_add_lshl_u32", 16: "v_xor_b32", 17: "v_add3_u32_sgpr", 18: "v_pk_add_u16",
-              19: "md5_mix_interleave8", 20: "md5_mix_interleave2", 21: "md5_mix_2add_interleave2"}
+              19: "md5_mix_interleave8", 20: "md5_mix_interleave2", 21: "md5_mix_2add_interleave2",
+              22: "md5_mix_alternating2", 23: "md5_mix_sgpr_k",
+              24: "md5_chain_compiler", 25: "md5_chain_alternating",
+              26: "alt_pairs_banks_distinct", 27: "alt_pairs_banks_same"}
 
 
 def valu_rate(device=0, kind=5):

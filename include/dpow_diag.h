@@ -17,7 +17,13 @@ extern "C" {
  *        11 v_or3_b32, 12 v_add_u32 with a literal, 13 v_alignbyte_b32, 14 v_bfi_b32,
  *        15 v_add_lshl_u32, 16 v_xor_b32, 17 v_add3_u32 with an SGPR operand, 18 v_pk_add_u16,
  *        19 the MD5 step mix interleaved across all 8 chains per instruction, 20 the same
- *        interleaved across pairs of chains, 21 as 20 with two v_add_u32 instead of v_add3_u32.
+ *        interleaved across pairs of chains, 21 as 20 with two v_add_u32 instead of v_add3_u32,
+ *        22 two chains software-pipelined so full- and half-rate instructions alternate,
+ *        23 the step mix with the v_add3_u32 constant in an SGPR (as the kernel issues it),
+ *        24 two candidates with MD5's real dependencies (4 state words each), compiler order,
+ *        25 the same in the search kernel's hand-ordered alternating groups,
+ *        26/27 kind 22's pattern on fixed registers whose operands sit in distinct / the
+ *        same VGPR bank (register index mod 4).
  * *lane_ops_per_s = wave64 instructions x 64 / s; *clock_ghz = mean in-kernel
  * shader clock (s_memtime / s_memrealtime).  Returns 0, or < 0 on error. */
 int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz);

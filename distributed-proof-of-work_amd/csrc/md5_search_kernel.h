@@ -98,15 +98,17 @@ DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &
 // ---------------------------------------------------------------------------
 // Two candidates, issue order fixed by hand.  Each MD5 step is four VALU
 // instructions, two full rate (v_bitop3_b32, v_add_u32) and two half rate
-// (v_add3_u32, v_alignbit_b32).  gfx950 issues this mix ~6 % faster when full-
-// and half-rate instructions strictly alternate than in the compiler's order
-// (dpow_diag_valu_rate kinds 5/20/22: 44.1 / 43.0 / 46.9 T lane-op/s), so
-// candidate q runs half a step behind candidate p and each step pair issues
+// (v_add3_u32, v_alignbit_b32).  Candidate q runs half a step behind
+// candidate p, so full- and half-rate instructions alternate and only a rotate
+// sits right before the instruction that reads it (dpow_diag_valu_rate kinds
+// 20-27, profiles/r01_valu_probe_order.log); each step pair issues
 //   F bop p(I) | H rot q(I-1) | F add q(I-1) | H add3 p(I) | F bop q(I) | H rot p(I) | F add p(I) | H add3 q(I)
-// One asm statement per step pair: the compiler keeps the order, allocates the
-// registers and places the SALU moves of the K constants, and inserts no
-// hazard padding inside the group (these plain VALU ops are interlocked in
-// hardware; per-instruction asm statements got an s_nop after every VOP3).
+// with s_nop padding (below) after the half-rate ones.  One asm statement per
+// step pair: the compiler keeps the order, allocates the registers and places
+// the SALU moves of the K constants, and adds no padding of its own inside the
+// group (these plain VALU ops are interlocked in hardware; one asm statement
+// per instruction got a conservative s_nop after every VOP3).  Together with
+// the padding: 170 -> 209 GH/s against the compiler-scheduled loop.
 namespace pipe {
 
 template <int I>

@@ -150,6 +150,19 @@ def main():
         tts[f"{bytes(nonce).hex()}/{n}"] = {"ms": round(dt * 1e3, 3), "global_idx": res.global_idx,
                                             "secret": list(res.secret)}
 
+    # Secondary sweep: the whole L = 3 chunk segment, k in [2^16, 2^24),
+    # one variable message word; and the early-exit latency of a Found/Cancel (worker.go:194,209).
+    extra = {}
+    if not args.no_tts:
+        barrier()
+        miner.reset_stats()
+        assert miner.search(NONCE, SWEEP_NTZ, wb, wbits, 1 << 16, 1 << 24).status == distpow.EXHAUSTED
+        s3 = miner.stats()
+        extra["secondary_sweep"] = {
+            "workload": "L=3 chunk segment, k in [2^16, 2^24), this rank's partition, N=32",
+            "candidates": int(s3.candidates), "kernel_ghs": round(s3.candidates / (s3.kernel_ms * 1e-3) / 1e9, 3)}
+        extra["cancel_latency_ms"] = cancel_latency(miner)
+
     probe = {}
     if rank == 0 and not args.no_probe:
         from distpow._lib import VALU_KINDS, valu_rate
@@ -210,6 +223,7 @@ def main():
             "stream_event_ms": round(stream_ms, 3),
             "valu_probe": probe,
             "time_to_secret": tts,
+            **extra,
             "cpu_baseline": cpu,
             "geometry": {"cus": cus, "threads_per_block": tpb},
         }
@@ -217,6 +231,27 @@ def main():
     miner.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def cancel_latency(miner, reps=3, run_s=0.05):
+    """Median ms from raising the pinned cancel flag (what Found/Cancel do, worker.go:194,209)
+    to dpow_search returning CANCELLED, mid-way through a 2.8e14-candidate window."""
+    import threading
+    lat = []
+    for _ in range(reps):
+        out = {}
+        th = threading.Thread(target=lambda: out.update(
+            r=miner.search(NONCE, SWEEP_NTZ, 0, 0, K0, 1 << 40), t=time.perf_counter()))
+        th.start()
+        time.sleep(run_s)
+        t0 = time.perf_counter()
+        miner.cancel()
+        th.join(timeout=30)
+        miner.clear_cancel()
+        assert not th.is_alive() and out["r"].status == distpow.CANCELLED, out
+        lat.append((out["t"] - t0) * 1e3)
+    torch.cuda.synchronize()
+    return round(sorted(lat)[len(lat) // 2], 3)
 
 
 def cpu_baseline(threads, seconds):

@@ -38,7 +38,7 @@ SWEEP_NTZ = 32
 CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 K0 = 1 << 24                      # start of the L = 4 segment
 PROFILE_TAG = "r01"                # profiles/<tag>_summary.json of the current kernel
-TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x16 up to 2^24 k
+TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x4 up to 2^22 k
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
 # INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,
 # the MI355X_MICROARCH.md FP32 vector peak (157.3 TFLOP/s) / 2 FLOP per FMA lane-op.

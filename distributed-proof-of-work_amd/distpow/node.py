@@ -48,18 +48,18 @@ def owner_rank(global_idx: int, world: int) -> int:
 
 def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
               batch_k: int = 1 << 8, k_start: int = 0, k_limit: int = DPOW_K_LIMIT, group=None,
-              device=None, cancelled: Callable[[], bool] = lambda: False, growth: int = 16,
-              batch_k_max: int = 1 << 24) -> NodeResult:
+              device=None, cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
+              batch_k_max: int = 1 << 22) -> NodeResult:
     """Search until the first hit of the whole node (deterministic) or a cancel vote.
 
     search_fn(nonce, ntz, worker_byte, worker_bits, k_begin, k_end, bound) -> SearchResult
     is this rank's one-window search (Miner.search for the GPU product).
 
-    Batches start at batch_k chunks and grow by `growth` up to batch_k_max: every rank
-    must finish a batch before the all-reduce, so small first batches keep the
-    time-to-secret of small N at one short batch, and large later ones keep the
-    per-batch all-reduce (~tens of us) under ~2 % of a batch (2^24 k x 32 thread bytes
-    at 8 GPUs = 2.6 ms of hashing per rank).
+    Batches start at batch_k chunks and grow by `growth` up to batch_k_max.  Every rank
+    must finish a batch before the all-reduce, so a batch bounds the overshoot past the
+    hit: small first batches keep small N at a few short batches, and the cap keeps
+    the overshoot at large N to one batch (2^22 k x 32 thread bytes at 8 GPUs = 0.65 ms
+    of hashing per rank), ~10x the per-batch all-reduce and host round trip.
     """
     import torch
     import torch.distributed as dist

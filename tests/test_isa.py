@@ -1,0 +1,59 @@
+"""Static checks of the gfx950 code the search kernel compiles to (no GPU needed).
+
+The hash loop's speed rests on its instruction stream: the
+hand-ordered two-candidate pipeline alternating full-rate (bitop3, add) and
+half-rate (add3, alignbit) VALU, s_nop padding after each half-rate instruction,
+and no SGPR-spill reloads.  A compiler or source change that silently breaks any
+of these costs 5-25 % of throughput; these tests catch it at build time.
+"""
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+pytestmark = pytest.mark.skipif(not shutil.which("/opt/rocm/bin/hipcc"), reason="hipcc not available")
+
+
+@pytest.fixture(scope="module")
+def kernel_110():
+    import isa_loop
+    text = isa_loop.disasm(os.path.join(ROOT, "distributed-proof-of-work_amd", "csrc"), 1, 0, [])
+    return isa_loop, isa_loop.kernel_lines(text, 1, 1, 0)
+
+
+def _kinds(lines):
+    m = {"v_bitop3_b32": "F", "v_add_u32_e32": "F", "v_add3_u32": "H", "v_alignbit_b32": "H", "s_nop": "n"}
+    out = []
+    for l in lines:
+        if re.search(r"//\s*[0-9A-F]{6,}:", l):
+            out.append(m.get(l.split()[0], "."))
+    return "".join(out)
+
+
+def test_hash_block_instruction_mix(kernel_110):
+    isa_loop, lines = kernel_110
+    blocks = isa_loop.hash_block_mix(lines)
+    assert blocks, "no hash block found"
+    lo, hi, c = max(blocks, key=lambda b: sum(b[2].values()))
+    valu = sum(v for k, v in c.items() if k.startswith("v_") and "lane" not in k)
+    assert 490 <= valu <= 505, valu                       # ~4 VALU per MD5 step x 2 candidates
+    assert c["v_alignbit_b32"] >= 120 and c["v_add3_u32"] >= 110
+    assert c.get("v_readlane_b32", 0) + c.get("v_writelane_b32", 0) <= 4  # SGPR budget holds
+    assert c.get("s_nop", 0) >= 200                        # padding after rotates and add3s
+
+
+def test_pipeline_alternates_full_and_half_rate(kernel_110):
+    _, lines = kernel_110
+    seq = _kinds(lines).replace(".", "")
+    # one padded step pair: F H n F H n F H n F H n (rotate and add3 each followed by s_nop)
+    group = "FHnFHnFHnFHn"
+    assert seq.count(group) >= 50, seq[:400]
+    # no half-rate instruction is directly followed by another VALU inside the pipeline
+    body = seq[seq.find(group):seq.rfind(group) + len(group)]
+    assert "HF" not in body and "HH" not in body

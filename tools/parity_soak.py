@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Randomised parity soak of the GPU search against the C oracle (test infrastructure).
+
+    python tools/parity_soak.py [seconds] [seed]
+
+Random nonce lengths (0..130, every kernel layout), partitions (workerBits 0..10),
+windows (every chunk-length segment, straddling segment / 2^24 boundaries) and
+trailing-zero counts (1..5); every GPU answer must equal the oracle's first hit
+(or "no hit").  Prints one JSON line with the case count.  GPU box only.
+"""
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "distributed-proof-of-work_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import torch  # noqa: F401,E402
+import distpow  # noqa: E402
+from _oracle import Oracle  # noqa: E402
+
+secs = float(sys.argv[1]) if len(sys.argv) > 1 else 60.0
+seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+rnd = random.Random(seed)
+o = Oracle()
+n_cases = hits = 0
+t_end = time.time() + secs
+with distpow.Miner(0) as m:
+    while time.time() < t_end:
+        nlen = rnd.randrange(131)
+        nonce = [rnd.randrange(256) for _ in range(nlen)]
+        wbits = rnd.choice([0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+        wb = rnd.randrange(1 << (wbits % 9)) if wbits % 9 else rnd.randrange(256)
+        rb = 8 - wbits % 9
+        ntz = rnd.choice([1, 2, 3, 3, 4, 4, 5])
+        seg = rnd.choice([0, 1, 2, 3, 4, 5])
+        k0 = rnd.randrange(1 << (8 * seg)) if seg else 0
+        if seg >= 2 and rnd.random() < 0.3:
+            k0 = max(0, (1 << (8 * seg)) - rnd.randrange(1, 64))
+        if seg >= 4 and rnd.random() < 0.3:
+            k0 = max(0, ((k0 >> 24) + 1 << 24) - rnd.randrange(1, 64))
+        nk = max(1, rnd.randrange(1, 1 + (1 << 17) // (1 << rb)))
+        k1 = min(k0 + nk, 1 << 40)
+        exp = o.mine_window(nonce, ntz, wb, wbits, k0, k1)
+        r = m.search(nonce, ntz, wb, wbits, k0, k1)
+        case = (nlen, nonce[:8], ntz, wb, wbits, k0, k1)
+        if exp is None:
+            assert r.status == distpow.EXHAUSTED, (case, r)
+        else:
+            assert r.status == distpow.FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1]), (case, r, exp)
+            hits += 1
+        n_cases += 1
+print(json.dumps({"cases": n_cases, "hits": hits, "seed": seed, "seconds": secs}))

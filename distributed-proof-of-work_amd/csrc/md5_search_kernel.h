@@ -1,27 +1,29 @@
-// md5_search.hip -- the gfx950 proof-of-work search kernel.
+// md5_search_kernel.h -- the gfx950 proof-of-work search kernel (instantiated
+// per message layout by md5_variant.hip).
 //
 // Replaces the reference miner's inner loop (worker.go:318-400): for every
 // candidate threadByte || chunk_k of the worker partition, MD5(nonce || it) and
 // the trailing-'0' test of its hex form.  Pure INT32 VALU work: each lane runs
-// an unrolled, register-resident MD5 of the final message block(s) of kNC
-// candidates (interleaved for ILP), the message words being wave-uniform
-// (kernel arguments, SGPRs) except the 4 bytes threadByte | k_lo << 8.
+// an unrolled, register-resident MD5 of the final message block(s) of two
+// candidates, software-pipelined in hand-ordered asm groups (see pipe::), the
+// message words being wave-uniform (kernel arguments, SGPRs) except the 4 bytes
+// threadByte | k_lo << 8.
 //
 // Work decomposition: local index i = k * R + t (the reference's order, k outer,
 // t inner).  A wave-block is 64 * kNC consecutive indices (lane l, slot j ->
 // i0 + 64 j + l).  Worker waves of a persistent grid claim chunks of
-// consecutive wave-blocks from an atomic counter, in increasing order; the
-// first hit of a wave-block (lowest slot, then lowest lane) goes to
+// consecutive wave-blocks from 8 per-XCD counters, each in increasing order;
+// the first hit of a wave-block (lowest slot, then lowest lane) goes to
 // atomicMin on the global index g = k * 256 + threadByte, which is monotone in
 // i, so the minimum is the reference's first hit.  A wave stops at the first
-// wave-block whose first index is >= the current minimum, so every candidate
-// below the answer is evaluated and the result is deterministic.
+// chunk whose first index is >= the current minimum, so every candidate below
+// the answer is evaluated and the result is deterministic.
 //
-// Workgroup 0 of the grid is a watcher: one lane polls the pinned host
-// cancel flag (Found/Cancel, worker.go:194,209) and raises Ctrl::stop, which
-// every worker wave reads once per chunk together with Ctrl::best; when the
-// last worker wave retires it writes the launch's completion record (Snap)
-// to pinned host memory, which the host polls.
+// Workgroup 0 of the grid is a watcher: one lane polls the pinned host cancel
+// flag (Found/Cancel, worker.go:194,209) and raises Ctrl::stop, which every
+// worker wave reads once per chunk together with Ctrl::best.  The workgroup that
+// retires last writes the launch's completion record (Snap) to pinned host
+// memory, which the host polls.
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -36,6 +36,7 @@ from distpow.node import NodeResult, node_mine, partition_of_rank  # noqa: E402
 NONCE = [1, 2, 3, 4]
 SWEEP_NTZ = 32
 CANDIDATES_PER_GPU_PER_STEP = 1 << 36
+STRONG_TOTAL_PER_STEP = 1 << 38    # --strong: fixed total work per step
 K0 = 1 << 24                      # start of the L = 4 segment
 PROFILE_TAG = "r01"                # profiles/<tag>_summary.json of the current kernel
 TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x4 up to 2^22 k
@@ -61,6 +62,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (gloo + --same-device only to rehearse the N>1 path on one GPU)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: 2^38 candidates per step in total, split over the ranks "
+                         "(default: weak, 2^36 per GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank searches on device 0 (with --backend gloo)")
     args = ap.parse_args()
@@ -79,7 +83,8 @@ def main():
             dist.init_process_group("gloo")
     wb, wbits = partition_of_rank(rank, world)
     R = 1 << (8 - wbits)
-    batch_k = CANDIDATES_PER_GPU_PER_STEP // R  # same k-window on every rank
+    per_gpu = (STRONG_TOTAL_PER_STEP // world) if args.strong else CANDIDATES_PER_GPU_PER_STEP
+    batch_k = per_gpu // R  # same k-window on every rank
 
     miner = distpow.Miner(device)
     dev = torch.device("cuda", device) if args.backend == "nccl" else torch.device("cpu")
@@ -123,7 +128,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
-    total_candidates = world * CANDIDATES_PER_GPU_PER_STEP * args.steps
+    total_candidates = world * per_gpu * args.steps
     value = total_candidates / elapsed_max / 1e9
     # roofline of the dominant (only) kernel: algorithmic ops per launch / avg launch duration
     avg_launch_ms = st.kernel_ms / max(1, st.launches)
@@ -195,14 +200,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
             "config": {
-                "workload": "sweep: nonce [1,2,3,4], 32 trailing zeros (unreachable), 2^36 candidates per GPU "
-                            "per step in the L=4 chunk segment (k >= 2^24); per-step RCCL MIN all-reduce",
-                "nonce": NONCE, "ntz": SWEEP_NTZ, "candidates_per_gpu_per_step": CANDIDATES_PER_GPU_PER_STEP,
+                "workload": "sweep: nonce [1,2,3,4], 32 trailing zeros (unreachable), "
+                            + ("2^38 candidates per step over all GPUs" if args.strong else "2^36 candidates per GPU per step")
+                            + " in the L=4 chunk segment (k >= 2^24); per-step RCCL MIN all-reduce",
+                "nonce": NONCE, "ntz": SWEEP_NTZ, "candidates_per_gpu_per_step": per_gpu,
                 "k_window_per_step": batch_k, "parallelism": f"prefix-partition x{world} (workerBits={wbits})",
             },
             "per_gpu_ghs": round(value / world, 3),

@@ -168,6 +168,9 @@ def main():
             "candidates": int(s3.candidates), "kernel_ghs": round(s3.candidates / (s3.kernel_ms * 1e-3) / 1e9, 3)}
         extra["cancel_latency_ms"] = cancel_latency(miner)
 
+    if rank == 0 and world == 1 and not args.no_tts:
+        extra["coordinator"] = coordinator_configs()
+
     probe = {}
     if rank == 0 and not args.no_probe:
         from distpow._lib import VALU_KINDS, valu_rate
@@ -237,6 +240,44 @@ def main():
     miner.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def coordinator_configs():
+    """BASELINE configs 3-5 end to end through the coordinator mirror (coordinator.go:139-320)
+    over native workers (worker.go:169-232), all logical workers on this rank's GPU: wall ms
+    per client request, first-arrived answers as the reference gives them, each verified."""
+    import threading
+    from distpow.coordinator import Coordinator
+
+    def timed(c, nonce, n):
+        t = time.perf_counter()
+        s = c.mine(nonce, n)
+        assert distpow.verify(nonce, s, n)
+        return round((time.perf_counter() - t) * 1e3, 3)
+
+    out = {}
+    with Coordinator(4) as c:  # config 3: 4 workers (workerBits = 2), N = 7, cold then warm cache
+        out["config3_4workers_n7_cold_ms"] = timed(c, [1, 2, 3, 4], 7)
+        out["config3_4workers_n7_warm_ms"] = timed(c, [1, 2, 3, 4], 7)
+    with Coordinator(8) as c:  # config 4: 8 workers (workerBits = 3), N = 8
+        out["config4_8workers_n8_ms"] = timed(c, [1, 2, 3, 4], 8)
+    with Coordinator(4) as c:  # config 5: two concurrent clients (cmd/client/main.go:40-51)
+        reqs = [([1, 2, 3, 4], 7), ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5), ([2, 2, 2, 2], 7)]
+        done = {}
+
+        def client(i, items):
+            for nonce, n in items:
+                done[(i, n, bytes(nonce))] = timed(c, nonce, n)
+
+        t = time.perf_counter()
+        th = [threading.Thread(target=client, args=(0, reqs[:2])), threading.Thread(target=client, args=(1, reqs[2:]))]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        assert len(done) == 4
+        out["config5_two_clients_total_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+    return out
 
 
 def cancel_latency(miner, reps=3, run_s=0.05):

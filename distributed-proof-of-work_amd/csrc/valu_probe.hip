@@ -38,6 +38,9 @@ __device__ __forceinline__ void op(uint32_t &a, uint32_t b, uint32_t c) {
     if constexpr (KIND == 16) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b));
     if constexpr (KIND == 17) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "s"(b), "v"(c));
     if constexpr (KIND == 18) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (KIND == 28) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 29) asm volatile("v_dot2_u32_u16 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (KIND == 30) asm volatile("v_bitop3_b16 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
 }
 
 template <int KIND>
@@ -175,6 +178,17 @@ __global__ void __launch_bounds__(kThreads) valu_probe_kernel(uint32_t *out, uin
                     asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[j]) : "v"(f), "s"(k));
                     asm volatile("v_alignbit_b32 %0, %0, %0, 25" : "+v"(x[j]));
                     asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j]) : "v"(b));
+                } else if constexpr (KIND == 31 || KIND == 32 || KIND == 33) {
+                    // 64-bit shifts / shift-add and the packed 64-bit move, on register pairs
+                    if (j % 2 == 0) {
+                        uint64_t v64 = ((uint64_t)x[j + 1] << 32) | x[j];
+                        const uint64_t w64 = ((uint64_t)b << 32) | c;
+                        if constexpr (KIND == 31) asm volatile("v_lshlrev_b64 %0, 7, %0" : "+v"(v64));
+                        if constexpr (KIND == 32) asm volatile("v_lshl_add_u64 %0, %0, 7, %1" : "+v"(v64) : "v"(w64));
+                        if constexpr (KIND == 33) asm volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]" : "+v"(v64) : "v"(w64));
+                        x[j] = (uint32_t)v64;
+                        x[j + 1] = (uint32_t)(v64 >> 32);
+                    }
                 } else if constexpr (KIND == 5) {
                     uint32_t f = x[j];
                     asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(f) : "v"(x[j]), "v"(b), "v"(c));
@@ -208,7 +222,7 @@ hipError_t run(uint32_t blocks, uint32_t iters, uint32_t *out, uint64_t *clk, hi
 }  // namespace
 
 extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz) {
-    if (kind < 0 || kind > 27 || !lane_ops_per_s || !clock_ghz) return -1;
+    if (kind < 0 || kind > 33 || !lane_ops_per_s || !clock_ghz) return -1;
     if (hipSetDevice(device) != hipSuccess) return -2;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -2;
@@ -252,7 +266,13 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             case 24: return run<24>(blocks, iters, out, clk, s);
             case 25: return run<25>(blocks, iters, out, clk, s);
             case 26: return run<26>(blocks, iters, out, clk, s);
-            default: return run<27>(blocks, iters, out, clk, s);
+            case 27: return run<27>(blocks, iters, out, clk, s);
+            case 28: return run<28>(blocks, iters, out, clk, s);
+            case 29: return run<29>(blocks, iters, out, clk, s);
+            case 30: return run<30>(blocks, iters, out, clk, s);
+            case 31: return run<31>(blocks, iters, out, clk, s);
+            case 32: return run<32>(blocks, iters, out, clk, s);
+            default: return run<33>(blocks, iters, out, clk, s);
         }
     };
     hipError_t err = hipSuccess;
@@ -274,7 +294,7 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             ++n;
         }
     const double instr_per_lane =
-        (double)iters * kUnroll * kChains * (kind == 5 || kind == 19 || kind == 20 || kind >= 22 ? 4 : kind == 21 ? 5 : 1);
+        (double)iters * kUnroll * kChains * (kind == 5 || kind == 19 || kind == 20 || (kind >= 22 && kind <= 27) ? 4 : kind == 21 ? 5 : kind >= 31 ? 0.5 : 1);
     *lane_ops_per_s = instr_per_lane * (double)blocks * kThreads * reps / (ms * 1e-3);
     *clock_ghz = n ? ratio / n * 0.1 : 0.0;  // s_memrealtime ticks at 100 MHz
     (void)hipFree(out);

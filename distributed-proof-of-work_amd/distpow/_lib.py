@@ -127,7 +127,9 @@ VALU_KINDS = {0: "v_add_u32", 1: "v_add3_u32", 2: "v_alignbit_b32", 3: "v_bitop3
               19: "md5_mix_interleave8", 20: "md5_mix_interleave2", 21: "md5_mix_2add_interleave2",
               22: "md5_mix_alternating2", 23: "md5_mix_sgpr_k",
               24: "md5_chain_compiler", 25: "md5_chain_alternating",
-              26: "alt_pairs_banks_distinct", 27: "alt_pairs_banks_same"}
+              26: "alt_pairs_banks_distinct", 27: "alt_pairs_banks_same", 28: "v_mad_u32_u24",
+              29: "v_dot2_u32_u16", 30: "v_bitop3_b16", 31: "v_lshlrev_b64", 32: "v_lshl_add_u64",
+              33: "v_pk_mov_b32"}
 
 
 def valu_rate(device=0, kind=5):

@@ -23,7 +23,9 @@ extern "C" {
  *        24 two candidates with MD5's real dependencies (4 state words each), compiler order,
  *        25 the same in the search kernel's hand-ordered alternating groups,
  *        26/27 kind 22's pattern on fixed registers whose operands sit in distinct / the
- *        same VGPR bank (register index mod 4).
+ *        same VGPR bank (register index mod 4), 28 v_mad_u32_u24, 29 v_dot2_u32_u16,
+ *        30 v_bitop3_b16, 31 v_lshlrev_b64, 32 v_lshl_add_u64, 33 v_pk_mov_b32 (31-33 count
+ *        one instruction per register pair).
  * *lane_ops_per_s = wave64 instructions x 64 / s; *clock_ghz = mean in-kernel
  * shader clock (s_memtime / s_memrealtime).  Returns 0, or < 0 on error. */
 int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz);

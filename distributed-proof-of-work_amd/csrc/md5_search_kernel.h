@@ -100,17 +100,16 @@ DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &
 // ---------------------------------------------------------------------------
 // Two candidates, issue order fixed by hand.  Each MD5 step is four VALU
 // instructions, two full rate (v_bitop3_b32, v_add_u32) and two half rate
-// (v_add3_u32, v_alignbit_b32).  Candidate q runs half a step behind
-// candidate p, so full- and half-rate instructions alternate and only a rotate
-// sits right before the instruction that reads it (dpow_diag_valu_rate kinds
-// 20-27, profiles/r01_valu_probe_order.log); each step pair issues
-//   F bop p(I) | H rot q(I-1) | F add q(I-1) | H add3 p(I) | F bop q(I) | H rot p(I) | F add p(I) | H add3 q(I)
-// with s_nop padding (below) after the half-rate ones.  One asm statement per
-// step pair: the compiler keeps the order, allocates the registers and places
-// the SALU moves of the K constants, and adds no padding of its own inside the
-// group (these plain VALU ops are interlocked in hardware; one asm statement
-// per instruction got a conservative s_nop after every VOP3).  Together with
-// the padding: 170 -> 209 GH/s against the compiler-scheduled loop.
+// (v_add3_u32, v_alignbit_b32), strictly dependent within a candidate.
+// Candidate q runs half a step behind candidate p and the two chains alternate
+// instruction by instruction (DPOW_PIPE_ORDER below), with s_nop padding after
+// the half-rate instructions.  One asm statement per step pair: the compiler
+// keeps the order, allocates the registers and places the SALU moves of the K
+// constants, and adds no padding of its own inside the group (these plain VALU
+// ops are interlocked in hardware; one asm statement per instruction got a
+// conservative s_nop after every VOP3).  Against the compiler-scheduled loop:
+// 170 -> 214.7 GH/s.  The probes that led here are dpow_diag_valu_rate kinds
+// 20-27 (profiles/r01_valu_probe_order.log).
 namespace pipe {
 
 template <int I>
@@ -125,11 +124,14 @@ template <int I> struct Roles {
 // Wait states after each instruction kind of a group (-1: none).  A VALU
 // instruction issued right behind the one it depends on holds the SIMD's issue
 // for the whole dependency latency -- every wave on the SIMD waits -- while an
-// s_nop holds only its own wave and lets the other waves issue.  Measured on
-// the sweep (profiles/r01_ab_nop.log): no padding 170 GH/s; s_nop 0 after each
-// rotate (its add depends on it) 192.5; plus s_nop 0 / 1 / 2 / 3 after each
-// add3 200.7 / 203.6 / 209.1 / 205.4; s_nop 1 after the rotate instead 191;
-// any padding after the full-rate ops 168-185; no rotate padding 179-180.
+// s_nop holds only its own wave and lets the other waves issue; the padding
+// after the half-rate instructions pays even where nothing depends on them.
+// Measured on the sweep (order 1, profiles/r01_ab_nop.log): no padding 170 GH/s;
+// s_nop 0 after each rotate 192.5; plus s_nop 0 / 1 / 2 / 3 after each add3
+// 200.7 / 203.6 / 209.1 / 205.4; s_nop 1 after the rotate instead 191; any
+// padding after the full-rate ops 168-185; no rotate padding 179-180.  Order 2
+// (profiles/r01_ab_order.log): the same s_nop 0 / s_nop 2 is best, 214.7; no
+// padding 170.7; add3 padding 1 or 3: 210.
 #ifndef DPOW_NOP_B
 #define DPOW_NOP_B -1  // after v_bitop3_b32
 #endif
@@ -165,6 +167,17 @@ template <int I> struct Roles {
 #define DPOW_PAD_A ""
 #endif
 
+// Order of a step pair (B bop3, A add3, R rotate, D add; p at step I, q finishing
+// step I-1 then starting step I).  2 (default): p.B q.R p.A q.D p.R q.B p.D q.A --
+// the two chains strictly alternate, so every dependency is two instructions
+// apart (F H H F H F F H); 214.7 GH/s.  1: p.B q.R q.D p.A q.B p.R p.D q.A --
+// F and H strictly alternate, but each rotate sits right before its add;
+// 209.1 GH/s.  (Two pairs interleaved at NC = 4 with both properties, every
+// dependency >= 3 apart: 191 GH/s at best.  profiles/r01_ab_order.log.)
+#ifndef DPOW_PIPE_ORDER
+#define DPOW_PIPE_ORDER 2
+#endif
+#if DPOW_PIPE_ORDER == 1
 #define DPOW_PIPE_BODY                                                     \
     "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \
     "v_alignbit_b32 %[rq], %[tq], %[tq], %[sq]\n\t" DPOW_PAD_R            \
@@ -174,6 +187,17 @@ template <int I> struct Roles {
     "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R            \
     "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t" DPOW_PAD_D                    \
     "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
+#else
+#define DPOW_PIPE_BODY                                                     \
+    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \
+    "v_alignbit_b32 %[rq], %[tq], %[tq], %[sq]\n\t" DPOW_PAD_R            \
+    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A                \
+    "v_add_u32_e32 %[qb], %[qc], %[rq]\n\t" DPOW_PAD_D                    \
+    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R            \
+    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" DPOW_PAD_B \
+    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t" DPOW_PAD_D                    \
+    "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
+#endif
 
 #define DPOW_PIPE_PRO                                                      \
     "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \

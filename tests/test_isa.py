@@ -1,8 +1,8 @@
 """Static checks of the gfx950 code the search kernel compiles to (no GPU needed).
 
 The hash loop's speed rests on its instruction stream: the
-hand-ordered two-candidate pipeline alternating full-rate (bitop3, add) and
-half-rate (add3, alignbit) VALU, s_nop padding after each half-rate instruction,
+hand-ordered two-candidate pipeline (the two candidates' dependency chains
+interleaved instruction by instruction), s_nop padding after each half-rate instruction,
 and no SGPR-spill reloads.  A compiler or source change that silently breaks any
 of these costs 5-25 % of throughput; these tests catch it at build time.
 """
@@ -48,11 +48,12 @@ def test_hash_block_instruction_mix(kernel_110):
     assert c.get("s_nop", 0) >= 200                        # padding after rotates and add3s
 
 
-def test_pipeline_alternates_full_and_half_rate(kernel_110):
+def test_pipeline_order_and_padding(kernel_110):
     _, lines = kernel_110
     seq = _kinds(lines).replace(".", "")
-    # one padded step pair: F H n F H n F H n F H n (rotate and add3 each followed by s_nop)
-    group = "FHnFHnFHnFHn"
+    # one padded step pair in DPOW_PIPE_ORDER 2: p.B q.R p.A q.D p.R q.B p.D q.A
+    # = F H H F H F F H, each rotate and add3 followed by its s_nop
+    group = "FHnHnFHnFFHn"
     assert seq.count(group) >= 50, seq[:400]
     # no half-rate instruction is directly followed by another VALU inside the pipeline
     body = seq[seq.find(group):seq.rfind(group) + len(group)]

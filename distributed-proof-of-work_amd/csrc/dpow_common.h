@@ -92,6 +92,8 @@ struct Launch {
     uint32_t rbits;        // R = 1 << rbits threadBytes per k
     uint32_t base_tb;      // uint8(worker_byte << rbits)
     uint32_t dmask;        // mask on the final D word for min(ntz, 8) trailing nibbles
+    uint32_t dle;          // prefilter D <= dle: the even-nibble part of dmask (dmask == ~dle for even ntz)
+    uint32_t deq;          // D-equality kernels (one final block, ntz >= 8): D == 0 <=> state word == deq = -iv[3]
     uint32_t ntz;          // requested trailing zeros (full digest check when > 8)
     uint32_t done_target;  // Ctrl::done once this launch's worker workgroups have retired
     uint32_t chunk;        // wave-blocks per claim
@@ -112,6 +114,19 @@ DPOW_HD uint32_t tail_nibble_mask(uint32_t n) {
     for (uint32_t j = 0; j < n && j < 8; ++j) m |= 0xFu << pos[j];
     return m;
 }
+
+// The one-compare prefilter of the D-word test: (D & tail_nibble_mask(n)) == 0
+// implies D <= tail_prefilter_le(n).  For even n the two are equivalent (the
+// mask is the top 4n bits); for odd n the prefilter covers the top 4(n-1) bits
+// and the rare path re-tests the mask.
+DPOW_HD uint32_t tail_prefilter_le(uint32_t n) {
+    const uint32_t e = (n < 8 ? n : 8) & ~1u;  // even part
+    return e == 0 ? 0xFFFFFFFFu : e >= 8 ? 0u : (0xFFFFFFFFu >> (4 * e));
+}
+
+// Kernels with the D-equality test: one final block (D = iv[3] + state word)
+// and a test on the whole D word.
+DPOW_HD bool use_d_equality(uint32_t nblk, uint32_t ntz) { return nblk == 1 && ntz >= 8; }
 
 DPOW_HD uint32_t bswap32(uint32_t x) {
     return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);

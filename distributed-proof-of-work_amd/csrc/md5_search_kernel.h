@@ -296,9 +296,12 @@ DPOW_DEV void steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
 
 // Final-block compression(s) of NCAND candidates; returns the digest words.
 // With ONLY_D the last block stops after step 61, which writes D (steps 62-63
-// only feed A..C): out[3] is exact, out[0..2] are not computed.
-template <int NBLK, int W0, int SH, int NCAND, bool ONLY_D = false>
+// only feed A..C): out[3] is exact, out[0..2] are not computed.  With RAW_D
+// (one final block) out[3] is the state word without the chaining value:
+// D = iv[3] + out[3], which the D-equality test compares against -iv[3].
+template <int NBLK, int W0, int SH, int NCAND, bool ONLY_D = false, bool RAW_D = false>
 DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords &v) {
+    static_assert(!RAW_D || (ONLY_D && NBLK == 1), "RAW_D: D word of one final block");
     uint32_t x[4][kNC];
 #pragma unroll
     for (int j = 0; j < NCAND; ++j) {
@@ -315,7 +318,7 @@ DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords 
 #pragma unroll
     for (int j = 0; j < NCAND; ++j)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) out[w][j] = L.iv[w] + x[w][j];
+        for (int w = 0; w < 4; ++w) out[w][j] = (RAW_D && w == 3) ? x[w][j] : L.iv[w] + x[w][j];
     if constexpr (NBLK == 2) {
         constexpr int kEnd1 = ONLY_D ? 62 : 64;
 #pragma unroll
@@ -403,10 +406,18 @@ DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
 }
 
 // Hash one wave-block (64 * kNC consecutive local indices from i0) and publish
-// its first hit, if any, to Ctrl::best.  Returns the wave's updated best.
-template <int NBLK, int W0, int SH>
-DPOW_DEV unsigned long long hash_wave_block(const Launch &L, uint64_t i0, uint32_t lane, uint32_t loff,
-                                            unsigned long long best) {
+// its first hit, if any, to Ctrl::best.  Returns the hit's global index, or
+// kNoHitG.
+//
+// The per-candidate test is one compare: with EQ (one final block, ntz >= 8)
+// the raw state word against -iv[3] (D == 0, no add, no mask); otherwise
+// D <= dle, the even-nibble prefilter of the mask, which the rare path (a hit
+// in the wave, 16^-(ntz & ~1) per candidate) re-tests against the exact mask.
+constexpr uint64_t kNoHitG = ~0ull;
+
+template <int NBLK, int W0, int SH, bool EQ>
+DPOW_DEV uint64_t hash_wave_block(const Launch &L, uint64_t i0, uint32_t lane, uint32_t loff) {
+    static_assert(!EQ || NBLK == 1, "the D-equality test needs one final block");
     uint32_t vs[kNC];
     VarWords v;
 #pragma unroll
@@ -415,20 +426,21 @@ DPOW_DEV unsigned long long hash_wave_block(const Launch &L, uint64_t i0, uint32
         var_words<SH>(v, j, vs[j], loff);
     }
     uint32_t dig[4][kNC];
-    md5_tail<NBLK, W0, SH, kNC, true>(dig, L, v);  // only D is tested here
+    md5_tail<NBLK, W0, SH, kNC, true, EQ>(dig, L, v);  // only D is tested here
 
     uint64_t bal[kNC];
     uint64_t any = 0;
 #pragma unroll
     for (int j = 0; j < kNC; ++j) {
-        bal[j] = __ballot((dig[3][j] & L.dmask) == 0u);
+        bal[j] = EQ ? __ballot(dig[3][j] == L.deq) : __ballot(dig[3][j] <= L.dle);
         any |= bal[j];
     }
-    if (any != 0) {  // rare (16^-N per candidate): lowest valid slot, then lowest lane
+    if (any != 0) {  // rare: lowest valid slot, then lowest lane
 #pragma unroll
         for (int j = 0; j < kNC; ++j) {
             const uint64_t ij = i0 + 64u * j;
             uint64_t m = bal[j] & lane_range_mask((int64_t)(L.i_begin - ij), (int64_t)(L.i_end - ij));
+            if (!EQ && m != 0) m &= __ballot((dig[3][j] & L.dmask) == 0u);
             if (m != 0 && L.ntz > 8u) {
                 const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, vs[j], loff);
                 m = __ballot(ok);
@@ -436,14 +448,14 @@ DPOW_DEV unsigned long long hash_wave_block(const Launch &L, uint64_t i0, uint32
             if (m != 0) {
                 const uint64_t g = global_of_local(ij + (uint64_t)__builtin_ctzll(m), L.rbits, L.base_tb);
                 if (lane == 0) atomicMin(&L.ctrl->best, (unsigned long long)g);
-                return g < best ? g : best;
+                return g;
             }
         }
     }
-    return best;
+    return kNoHitG;
 }
 
-template <int NBLK, int W0, int SH>
+template <int NBLK, int W0, int SH, bool EQ>
 __global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR)))
 md5_search_kernel(const Launch L) {
     if (blockIdx.x == 0) {  // dispatched first: the watcher
@@ -501,9 +513,15 @@ md5_search_kernel(const Launch L) {
         const unsigned long long best_next =
             __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t stop_next = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // A hit ends the chunk: its later wave-blocks hold larger indices.
         uint64_t i0 = i_first;
-        for (uint32_t r = 0; r < nb; ++r, i0 += (uint64_t)kWaveBlock)
-            best = hash_wave_block<NBLK, W0, SH>(L, i0, lane, loff, best);
+        for (uint32_t r = 0; r < nb; ++r, i0 += (uint64_t)kWaveBlock) {
+            const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, i0, lane, loff);
+            if (g != kNoHitG) {
+                best = g < best ? g : best;
+                break;
+            }
+        }
         best = best_next < best ? best_next : best;
         stop = stop_next;
         claim = next;

@@ -1,6 +1,7 @@
 // md5_variant.hip -- instantiates md5_search_kernel for one (NBLK, SH) pair and
 // every word position W0 of that pair.  Compiled once per pair by the Makefile
-// (-DDPOW_VNBLK=<1|2> -DDPOW_VSH=<0..3>) so the 72 variants build in parallel.
+// (-DDPOW_VNBLK=<1|2> -DDPOW_VSH=<0..3>) so the 72 layouts (plus the 56
+// one-block D-equality kernels) build in parallel.
 #include "md5_search_kernel.h"
 #include "md5_variants.h"
 
@@ -15,19 +16,27 @@ namespace dpow {
 
 namespace {
 using KernelFn = void (*)(Launch);
-#define DPOW_K(w) md5_search_kernel<DPOW_VNBLK, w, DPOW_VSH>
+// [EQ][w0 - kW0Lo]: EQ kernels (the D-equality test, use_d_equality) exist for
+// one final block only.
+#define DPOW_K(w, e) md5_search_kernel<DPOW_VNBLK, w, DPOW_VSH, e>
 #if DPOW_VNBLK == 1
 constexpr int kW0Lo = 0;
-const KernelFn kTable[] = {DPOW_K(0), DPOW_K(1), DPOW_K(2),  DPOW_K(3),  DPOW_K(4),  DPOW_K(5),  DPOW_K(6),
-                           DPOW_K(7), DPOW_K(8), DPOW_K(9), DPOW_K(10), DPOW_K(11), DPOW_K(12), DPOW_K(13)};
+#define DPOW_ROW(e) \
+    {DPOW_K(0, e), DPOW_K(1, e), DPOW_K(2, e),  DPOW_K(3, e),  DPOW_K(4, e),  DPOW_K(5, e),  DPOW_K(6, e), \
+     DPOW_K(7, e), DPOW_K(8, e), DPOW_K(9, e), DPOW_K(10, e), DPOW_K(11, e), DPOW_K(12, e), DPOW_K(13, e)}
+const KernelFn kTable[2][14] = {DPOW_ROW(false), DPOW_ROW(true)};
 #else
 constexpr int kW0Lo = 12;
-const KernelFn kTable[] = {DPOW_K(12), DPOW_K(13), DPOW_K(14), DPOW_K(15)};
+#define DPOW_ROW(e) {DPOW_K(12, e), DPOW_K(13, e), DPOW_K(14, e), DPOW_K(15, e)}
+const KernelFn kTable[2][4] = {DPOW_ROW(false), DPOW_ROW(false)};
 #endif
+#undef DPOW_ROW
 #undef DPOW_K
-constexpr int kW0N = sizeof(kTable) / sizeof(kTable[0]);
+constexpr int kW0N = sizeof(kTable[0]) / sizeof(kTable[0][0]);
 
-KernelFn pick(int w0) { return (w0 >= kW0Lo && w0 < kW0Lo + kW0N) ? kTable[w0 - kW0Lo] : nullptr; }
+KernelFn pick(int w0, bool eq) {
+    return (w0 >= kW0Lo && w0 < kW0Lo + kW0N) ? kTable[eq ? 1 : 0][w0 - kW0Lo] : nullptr;
+}
 }  // namespace
 
 #define DPOW_CAT3(a, b, c) a##b##_##c
@@ -35,14 +44,14 @@ KernelFn pick(int w0) { return (w0 >= kW0Lo && w0 < kW0Lo + kW0N) ? kTable[w0 - 
 
 hipError_t DPOW_NAME(variant_launch_, DPOW_VNBLK, DPOW_VSH)(int w0, const Launch &L, uint32_t grid,
                                                            hipStream_t stream) {
-    KernelFn fn = pick(w0);
+    KernelFn fn = pick(w0, use_d_equality(DPOW_VNBLK, L.ntz));
     if (!fn) return hipErrorInvalidValue;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlockThreads), 0, stream, L);
     return hipGetLastError();
 }
 
 hipError_t DPOW_NAME(variant_occupancy_, DPOW_VNBLK, DPOW_VSH)(int w0, int *blocks_per_cu) {
-    KernelFn fn = pick(w0);
+    KernelFn fn = pick(w0, false);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void *>(fn),
                                                         kBlockThreads, 0);

@@ -91,6 +91,8 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     Lh.rbits = rbits_;
     Lh.base_tb = base_tb_;
     Lh.dmask = tail_nibble_mask(ntz_ < 8 ? ntz_ : 8);
+    Lh.dle = tail_prefilter_le(ntz_);
+    Lh.deq = 0u - iv_[3];
     Lh.ntz = ntz_;
     pl.info.k_begin = k;
     pl.info.k_end = ke;

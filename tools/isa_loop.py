@@ -33,8 +33,8 @@ def disasm(csrc, nblk, sh, extra):
     return subprocess.check_output([f"{LLVM}/llvm-objdump", "-d", co]).decode()
 
 
-def kernel_lines(text, nblk, w0, sh):
-    pat = re.compile(rf"md5_search_kernelILi{nblk}ELi{w0}ELi{sh}E.*>:")
+def kernel_lines(text, nblk, w0, sh, eq=0):
+    pat = re.compile(rf"md5_search_kernelILi{nblk}ELi{w0}ELi{sh}ELb{eq}E.*>:")
     out, on = [], False
     for line in text.splitlines():
         if pat.search(line):
@@ -110,17 +110,19 @@ def main():
     ap.add_argument("--nblk", type=int, default=1)
     ap.add_argument("--sh", type=int, default=0)
     ap.add_argument("--w0", default="1,0,2,3,13")
+    ap.add_argument("--eq", type=int, default=None, help="1: D-equality kernels (default for --nblk 1)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
     text = disasm(a.csrc, a.nblk, a.sh, a.extra)
+    eq = (1 if a.nblk == 1 else 0) if a.eq is None else a.eq
     for w0 in [int(x) for x in a.w0.split(",")]:
-        kl = kernel_lines(text, a.nblk, w0, a.sh)
+        kl = kernel_lines(text, a.nblk, w0, a.sh, eq)
         for lo, hi, c in hash_block_mix(kl) or []:
             valu = sum(v for k, v in c.items() if k.startswith("v_") and "lane" not in k)
             spill = c.get("v_readlane_b32", 0) + c.get("v_writelane_b32", 0)
             salu = sum(v for k, v in c.items() if k.startswith("s_"))
-            print(f"<{a.nblk},{w0},{a.sh}> hash block +0x{lo:x}..+0x{hi:x} (start mod 64 = {lo % 64}): "
+            print(f"<{a.nblk},{w0},{a.sh},eq{eq}> hash block +0x{lo:x}..+0x{hi:x} (start mod 64 = {lo % 64}): "
                   f"VALU {valu}  SALU {salu}  spill readlane/writelane {spill}")
             if a.verbose:
                 for k, v in c.most_common():

@@ -41,6 +41,14 @@ __device__ __forceinline__ void op(uint32_t &a, uint32_t b, uint32_t c) {
     if constexpr (KIND == 28) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
     if constexpr (KIND == 29) asm volatile("v_dot2_u32_u16 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
     if constexpr (KIND == 30) asm volatile("v_bitop3_b16 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
+    // SDWA halves of b + rot16(t): b + t.hi (32-bit add, src1 = WORD_1), then the
+    // top half += t.lo (16-bit add into WORD_1, low half preserved)
+    if constexpr (KIND == 34)
+        asm volatile("v_add_u32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+                     : "+v"(a) : "v"(b));
+    if constexpr (KIND == 35)
+        asm volatile("v_add_u16_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0"
+                     : "+v"(a) : "v"(b));
 }
 
 template <int KIND>
@@ -144,6 +152,43 @@ __global__ void __launch_bounds__(kThreads) valu_probe_kernel(uint32_t *out, uin
                             : [pb] "v"(x[bb]), [pc] "v"(x[cc]), [pd] "v"(x[d]), [qc] "v"(x[4 + cc]), [qd] "v"(x[4 + d]),
                               [qa] "v"(x[4 + a]), [kp] "s"(ks), [kq] "s"(ks));
                     }
+                } else if constexpr (KIND == 36 || KIND == 37) {
+                    // the search kernel's order-2 step pair with its padding; 37 replaces
+                    // each rotate + add by the two SDWA adds of b + rot16(t)
+                    if (j % 2 == 0) {
+                        const int I = 4 * u + j / 2;
+                        const int a = (64 - I) % 4, bb = (a + 1) % 4, cc = (a + 2) % 4, d = (a + 3) % 4;
+                        uint32_t fp, fq, rq, tp;
+                        if constexpr (KIND == 36)
+                            asm volatile(
+                                "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:0x96\n\t"
+                                "v_alignbit_b32 %[rq], %[tq], %[tq], 16\n\ts_nop 0\n\t"
+                                "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\ts_nop 2\n\t"
+                                "v_add_u32_e32 %[qb], %[qc], %[rq]\n\t"
+                                "v_alignbit_b32 %[tp], %[tp], %[tp], 16\n\ts_nop 0\n\t"
+                                "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:0x96\n\t"
+                                "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t"
+                                "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\ts_nop 2"
+                                : [pa] "+v"(x[a]), [qb] "=&v"(x[4 + bb]), [tq] "+v"(tqv), [fp] "=&v"(fp), [fq] "=&v"(fq),
+                                  [rq] "=&v"(rq), [tp] "=&v"(tp)
+                                : [pb] "v"(x[bb]), [pc] "v"(x[cc]), [pd] "v"(x[d]), [qc] "v"(x[4 + cc]),
+                                  [qd] "v"(x[4 + d]), [qa] "v"(x[4 + a]), [kp] "s"(ks), [kq] "s"(ks));
+                        else
+                            asm volatile(
+                                "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:0x96\n\t"
+                                "v_add_u32_sdwa %[qb], %[qc], %[tq] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+                                "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\ts_nop 2\n\t"
+                                "v_add_u16_sdwa %[qb], %[qb], %[tq] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t"
+                                "v_add_u32_sdwa %[pa], %[pb], %[tp] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+                                "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:0x96\n\t"
+                                "v_add_u16_sdwa %[pa], %[pa], %[tp] dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t"
+                                "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\ts_nop 2"
+                                : [pa] "+v"(x[a]), [qb] "=&v"(x[4 + bb]), [tq] "+v"(tqv), [fp] "=&v"(fp), [fq] "=&v"(fq),
+                                  [rq] "=&v"(rq), [tp] "=&v"(tp)
+                                : [pb] "v"(x[bb]), [pc] "v"(x[cc]), [pd] "v"(x[d]), [qc] "v"(x[4 + cc]),
+                                  [qd] "v"(x[4 + d]), [qa] "v"(x[4 + a]), [kp] "s"(ks), [kq] "s"(ks));
+                        (void)rq;
+                    }
                 } else if constexpr (KIND == 26 || KIND == 27) {
                     // kind 22's alternating pairs on fixed registers (4 pairs p/q = v24+4k / v25+4k):
                     // 26 reads operands from distinct VGPR banks (index mod 4), 27 from one bank
@@ -222,7 +267,7 @@ hipError_t run(uint32_t blocks, uint32_t iters, uint32_t *out, uint64_t *clk, hi
 }  // namespace
 
 extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz) {
-    if (kind < 0 || kind > 33 || !lane_ops_per_s || !clock_ghz) return -1;
+    if (kind < 0 || kind > 37 || !lane_ops_per_s || !clock_ghz) return -1;
     if (hipSetDevice(device) != hipSuccess) return -2;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -2;
@@ -272,6 +317,10 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             case 30: return run<30>(blocks, iters, out, clk, s);
             case 31: return run<31>(blocks, iters, out, clk, s);
             case 32: return run<32>(blocks, iters, out, clk, s);
+            case 34: return run<34>(blocks, iters, out, clk, s);
+            case 35: return run<35>(blocks, iters, out, clk, s);
+            case 36: return run<36>(blocks, iters, out, clk, s);
+            case 37: return run<37>(blocks, iters, out, clk, s);
             default: return run<33>(blocks, iters, out, clk, s);
         }
     };
@@ -294,7 +343,8 @@ extern "C" int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s,
             ++n;
         }
     const double instr_per_lane =
-        (double)iters * kUnroll * kChains * (kind == 5 || kind == 19 || kind == 20 || (kind >= 22 && kind <= 27) ? 4 : kind == 21 ? 5 : kind >= 31 ? 0.5 : 1);
+        (double)iters * kUnroll * kChains * (kind == 5 || kind == 19 || kind == 20 || (kind >= 22 && kind <= 27) || kind == 36 || kind == 37 ? 4
+         : kind == 21 ? 5 : (kind >= 31 && kind <= 33) ? 0.5 : 1);
     *lane_ops_per_s = instr_per_lane * (double)blocks * kThreads * reps / (ms * 1e-3);
     *clock_ghz = n ? ratio / n * 0.1 : 0.0;  // s_memrealtime ticks at 100 MHz
     (void)hipFree(out);

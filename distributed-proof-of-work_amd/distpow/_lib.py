@@ -129,7 +129,9 @@ VALU_KINDS = {0: "v_add_u32", 1: "v_add3_u32", 2: "v_alignbit_b32", 3: "v_bitop3
               24: "md5_chain_compiler", 25: "md5_chain_alternating",
               26: "alt_pairs_banks_distinct", 27: "alt_pairs_banks_same", 28: "v_mad_u32_u24",
               29: "v_dot2_u32_u16", 30: "v_bitop3_b16", 31: "v_lshlrev_b64", 32: "v_lshl_add_u64",
-              33: "v_pk_mov_b32"}
+              33: "v_pk_mov_b32",
+              34: "v_add_u32_sdwa_word1", 35: "v_add_u16_sdwa_dst_word1",
+              36: "md5_pair_rot16_alignbit", 37: "md5_pair_rot16_sdwa"}
 
 
 def valu_rate(device=0, kind=5):

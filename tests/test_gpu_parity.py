@@ -256,3 +256,47 @@ def test_small_launch_grids_vs_oracle(miner, oracle):
             else:
                 assert r.status == FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1]), \
                     (wbits, wb, k0, n, ntz, r, exp)
+
+
+def _secret_of(g):
+    k = g >> 8
+    return bytes([g & 255]) + k.to_bytes((k.bit_length() + 7) // 8, "little")
+
+
+def _tz(nonce, secret):
+    h = hashlib.md5(bytes(nonce) + bytes(secret)).hexdigest()
+    return len(h) - len(h.rstrip("0"))
+
+
+@pytest.mark.parametrize("nlen,wbits,wb", [(4, 0, 0), (11, 0, 0), (23, 0, 0), (46, 2, 3), (70, 0, 0),
+                                           (129, 3, 5), (60, 0, 0)])
+def test_n8_first_hit_vs_n7_walk(miner, nlen, wbits, wb):
+    """The N >= 8 kernels (one final block: the D-equality test, raw state word ==
+    -iv[3]) against the N = 7 kernels (prefilter D <= 0xFF + nibble mask), beyond the
+    oracle's reach: walking the N = 7 hits in order up to the N = 8 answer g8, every
+    candidate of every visited k below g8 (all of the partition's thread bytes, by
+    hashlib) has < 8 trailing zeros, and g8 has >= 8.  Nonce lengths cover the
+    plain, midstate (70, 129) and two-final-block (60) layouts."""
+    rnd = random.Random(nlen * 131 + wbits)
+    nonce = [1, 2, 3, 4] if nlen == 4 else [rnd.randrange(256) for _ in range(nlen)]
+    r8 = miner.mine(nonce, 8, wb, wbits)
+    assert r8.status == FOUND
+    g8 = r8.global_idx
+    assert bytes(r8.secret) == _secret_of(g8) and _tz(nonce, r8.secret) >= 8
+    rb = 8 - wbits % 9
+    tbs = [((wb << rb) | j) & 255 for j in range(1 << rb)]
+    k, kend, walked = 0, (g8 >> 8) + 1, 0
+    while True:
+        r7 = miner.search(nonce, 7, wb, wbits, k, kend)
+        assert r7.status == FOUND and r7.global_idx <= g8, (k, kend, r7)
+        assert _tz(nonce, r7.secret) >= 7
+        ks = r7.global_idx >> 8
+        for t in tbs:
+            g = (ks << 8) | t
+            if g < g8:
+                assert _tz(nonce, _secret_of(g)) < 8, (nonce, g, g8)
+        walked += 1
+        if ks == g8 >> 8:
+            break
+        k = ks + 1
+    assert walked >= 1

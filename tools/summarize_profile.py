@@ -72,6 +72,15 @@ def main():
             summary["waves_per_launch"] = avg["SQ_WAVES"]
             summary["pmc_launch_ms"] = avg["ms"]
             summary["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / (avg["ms"] * 1e-3) / 1e9
+            # VALU utilisation: wave64 VALU instructions issued per SIMD per cycle
+            # (GRBM_GUI_ACTIVE sums the 8 XCDs' cycles; 1024 SIMDs), and that rate
+            # weighted by the hash block's mix (tools/isa_loop.py: 236 half-rate
+            # instructions at 4 cycles + 258 full-rate at 2 cycles per 494), i.e.
+            # the fraction of SIMD cycles the VALU is busy under the 2/4-cycle model.
+            cyc = avg["GRBM_GUI_ACTIVE"] / 8
+            rate = avg["SQ_INSTS_VALU"] / 1024 / cyc
+            summary["valu_insts_per_simd_cycle"] = rate
+            summary["valu_busy_issue_model"] = rate * (236 * 4 + 258 * 2) / 494
         # FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM section): on gfx950
         # FETCH_SIZE reports half the bytes of coalesced reads (x2 before comparing with a byte
         # count); WRITE_SIZE is exact for streaming stores and one-dword atomics.  This kernel's

@@ -56,11 +56,80 @@ DPOW_DEV uint32_t md5_fn(uint32_t x, uint32_t y, uint32_t z) {
     return __builtin_amdgcn_bitop3_b32(x, y, z, tt);
 }
 
+// Launch-uniform K + M constants kept in VGPRs (every lane the same value).
+// Layouts with long nonces need up to ~50 distinct K + M constants in the
+// pipelined steps (every nonce word, four times per block).  Under the 80-SGPR
+// budget of 8 waves/SIMD the compiler spills them to VGPR lanes and reloads
+// each with a v_readlane -- a VALU instruction -- on every use (28-54 per
+// wave-block in the two-block kernels).  Copied once per wave into VGPRs with
+// an opaque v_mov (so they are not folded back to SGPRs), they cost nothing in
+// the loop: v_add3_u32 reads a VGPR operand at the same rate.  Capped so the
+// kernel stays within 64 VGPRs (8 waves/SIMD).
+#ifndef DPOW_VGPR_K
+#define DPOW_VGPR_K 1  // A/B switch
+#endif
+#ifndef DPOW_VGPR_K_MAX
+#define DPOW_VGPR_K_MAX -1  // >= 0: one cap for every layout (A/B); -1: VgprK::kCap
+#endif
+#ifndef DPOW_VGPR_K_MIN
+#define DPOW_VGPR_K_MIN 0  // layouts with fewer eligible constants keep them all in SGPRs
+#endif
+
+struct KConst {
+    uint32_t v[128];  // [64 * BLK + I]; only the entries VgprK selects are set
+};
+
+template <int NBLK, int W0, int SH>
+struct VgprK {
+    // First step of block 0 in the hand-ordered pipeline (md5_tail's kI0 for
+    // the hash loop's ONLY_D call with kNC candidates).
+    static constexpr int kEnd0 = NBLK == 1 ? 62 : 64;
+    static constexpr int kI0 = W0 + 4 < kEnd0 ? W0 + 4 : kEnd0;
+    static constexpr bool eligible(int blk, int i) {
+        const int m = 16 * blk + md5_word(i);
+        const bool zero = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
+        const bool lane = m == W0 || (SH != 0 && m == W0 + 1);
+        const bool piped = blk > 0 || i >= kI0;
+        const bool run = !(blk == NBLK - 1 && i >= 62);
+        return !zero && !lane && piped && run;
+    }
+    static constexpr int rank(int blk, int i) {
+        int r = 0;
+        for (int b = 0; b < NBLK; ++b)
+            for (int j = 0; j < 64; ++j) {
+                if (b == blk && j == i) return r;
+                if (eligible(b, j)) ++r;
+            }
+        return r;
+    }
+    static constexpr int count() { return rank(NBLK, 0); }
+    // VGPRs the layout uses without VGPR constants (-Rpass-analysis=kernel-resource-usage):
+    // one block 34-39 (SH = 0) / 43-49 (SH != 0), two blocks 41-43 / 49-53; each
+    // constant costs about one more.  The caps keep every kernel at <= 64.
+    static constexpr int kCap = DPOW_VGPR_K_MAX >= 0 ? DPOW_VGPR_K_MAX
+                                : NBLK == 1 ? (SH == 0 ? 24 : 14)
+                                            : (SH == 0 ? 20 : 10);
+    static constexpr bool use(int blk, int i) {
+        return DPOW_VGPR_K && count() >= DPOW_VGPR_K_MIN && eligible(blk, i) && rank(blk, i) < kCap;
+    }
+};
+
+template <int NBLK, int W0, int SH, int BLK, int I>
+DPOW_DEV void kconst_init(KConst &kc, const Launch &L) {
+    if constexpr (BLK < NBLK) {
+        if constexpr (VgprK<NBLK, W0, SH>::use(BLK, I))
+            asm("v_mov_b32 %0, %1" : "=v"(kc.v[64 * BLK + I]) : "s"(L.KT[64 * BLK + I]));
+        if constexpr (I + 1 < 64) kconst_init<NBLK, W0, SH, BLK, I + 1>(kc, L);
+        else kconst_init<NBLK, W0, SH, BLK + 1, 0>(kc, L);
+    }
+}
+
 // Per-candidate variable message parts.
 struct VarWords {
     uint32_t lo_s[kNC];  // wave-uniform part of V << 8*SH (word W0)
     uint32_t lo_v;       // per-lane part of V << 8*SH (the same for every slot)
     uint32_t hi[kNC];    // V >> (32 - 8*SH), added for steps reading word W0+1
+    const KConst *kc;    // launch-uniform K + M constants held in VGPRs
 };
 
 // K + M of step I of block BLK for candidate j (the message word M includes the
@@ -73,8 +142,9 @@ struct StepWord {
     // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
     static constexpr bool zero_word = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
     static constexpr bool per_lane = m == W0 || (SH != 0 && m == W0 + 1);
+    static constexpr bool vgpr_k = VgprK<NBLK, W0, SH>::use(BLK, I);
     static DPOW_DEV uint32_t km(const Launch &L, const VarWords &v, int j) {
-        uint32_t k = zero_word ? kMd5K[I] : L.KT[64 * BLK + I];
+        uint32_t k = zero_word ? kMd5K[I] : vgpr_k ? v.kc->v[64 * BLK + I] : L.KT[64 * BLK + I];
         if constexpr (m == W0) k = (k + v.lo_s[j]) + v.lo_v;
         if constexpr (SH != 0 && m == W0 + 1) k += v.hi[j];
         return k;
@@ -215,7 +285,7 @@ DPOW_DEV void body(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const V
     using W = StepWord<NBLK, W0, SH, BLK, I>;
     const uint32_t kp = W::km(L, v, J), kq = W::km(L, v, J + 1);
     uint32_t fp, fq, rq, tp;
-    if constexpr (W::per_lane)
+    if constexpr (W::per_lane || W::vgpr_k)
         asm volatile(DPOW_PIPE_BODY
                      : [pa] "+v"(x[R::a][J]), [qb] "=&v"(x[R::b][J + 1]), [tq] "+v"(tq), [fp] "=&v"(fp),
                        [fq] "=&v"(fq), [rq] "=&v"(rq), [tp] "=&v"(tp)
@@ -238,7 +308,7 @@ DPOW_DEV void prologue(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, con
     using W = StepWord<NBLK, W0, SH, BLK, I0>;
     const uint32_t kp = W::km(L, v, J), kq = W::km(L, v, J + 1);
     uint32_t fp, fq, tp;
-    if constexpr (W::per_lane)
+    if constexpr (W::per_lane || W::vgpr_k)
         asm volatile(DPOW_PIPE_PRO
                      : [pa] "+v"(x[R::a][J]), [tq] "=&v"(tq), [fp] "=&v"(fp), [fq] "=&v"(fq), [tp] "=&v"(tp)
                      : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qb] "v"(x[R::b][J + 1]),
@@ -347,8 +417,9 @@ DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff) {
 // Full digest test of one lane's candidate (rare path: only when the D-word
 // test passed and ntz > 8, i.e. probability 2^-32 per candidate).
 template <int NBLK, int W0, int SH>
-DPOW_DEV bool full_check(const Launch &L, uint32_t vs, uint32_t loff) {
+DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_t loff) {
     VarWords v;
+    v.kc = &kc;
     var_words<SH>(v, 0, vs, loff);
     uint32_t out[4][kNC];
     md5_tail<NBLK, W0, SH, 1>(out, L, v);
@@ -416,10 +487,11 @@ DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
 constexpr uint64_t kNoHitG = ~0ull;
 
 template <int NBLK, int W0, int SH, bool EQ>
-DPOW_DEV uint64_t hash_wave_block(const Launch &L, uint64_t i0, uint32_t lane, uint32_t loff) {
+DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0, uint32_t lane, uint32_t loff) {
     static_assert(!EQ || NBLK == 1, "the D-equality test needs one final block");
     uint32_t vs[kNC];
     VarWords v;
+    v.kc = &kc;
 #pragma unroll
     for (int j = 0; j < kNC; ++j) {
         vs[j] = wave_uniform_v(i0 + 64u * j, L.rbits, L.base_tb);
@@ -442,7 +514,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, uint64_t i0, uint32_t lane, u
             uint64_t m = bal[j] & lane_range_mask((int64_t)(L.i_begin - ij), (int64_t)(L.i_end - ij));
             if (!EQ && m != 0) m &= __ballot((dig[3][j] & L.dmask) == 0u);
             if (m != 0 && L.ntz > 8u) {
-                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, vs[j], loff);
+                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, kc, vs[j], loff);
                 m = __ballot(ok);
             }
             if (m != 0) {
@@ -464,6 +536,8 @@ md5_search_kernel(const Launch L) {
     }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t loff = lane_offset(L.rbits, lane);
+    KConst kc;
+    kconst_init<NBLK, W0, SH, 0, 0>(kc, L);
 
     unsigned long long best = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t stop = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -516,7 +590,7 @@ md5_search_kernel(const Launch L) {
         // A hit ends the chunk: its later wave-blocks hold larger indices.
         uint64_t i0 = i_first;
         for (uint32_t r = 0; r < nb; ++r, i0 += (uint64_t)kWaveBlock) {
-            const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, i0, lane, loff);
+            const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, kc, i0, lane, loff);
             if (g != kNoHitG) {
                 best = g < best ? g : best;
                 break;

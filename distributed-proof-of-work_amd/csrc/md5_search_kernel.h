@@ -48,6 +48,13 @@ namespace dpow {
 #ifndef DPOW_NUM_SGPR
 #define DPOW_NUM_SGPR 72
 #endif
+// A wave polls Ctrl::best / Ctrl::stop every DPOW_POLL_WB wave-blocks of a
+// chunk (0: once per chunk).  profiles/r01_ab_poll.log: 0 / 12 / 16 / 32 ->
+// 216.3 / 217.8 / 218.3 / 218.6 GH/s, time-to-secret N=7 1.57 / 1.47 / 1.49 / 1.56 ms.
+#ifndef DPOW_POLL_WB
+#define DPOW_POLL_WB 16
+#endif
+constexpr uint32_t kPollWb = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 1;
 
 template <int I>
 DPOW_DEV uint32_t md5_fn(uint32_t x, uint32_t y, uint32_t z) {
@@ -583,6 +590,35 @@ md5_search_kernel(const Launch L) {
         if (stop != 0u ||
             global_of_local(i_first < L.i_begin ? L.i_begin : i_first, L.rbits, L.base_tb) >= best)
             break;
+#if DPOW_POLL_WB > 0
+        // The chunk runs in groups of kPollWb wave-blocks.  Each group's loads of
+        // Ctrl::best / Ctrl::stop are issued before it and consumed after it (the
+        // latency hides behind the hashing), so a hit elsewhere or a cancel ends
+        // this wave within one group, not at the chunk's end.  A hit of this wave
+        // ends the chunk at once: its later wave-blocks hold larger indices.
+        // Down-counters keep the loop's live SGPRs at a plain loop's count.
+        uint64_t i0 = i_first;
+        uint32_t left = nb;
+        for (;;) {
+            uint32_t q = left < kPollWb ? left : kPollWb;
+            left -= q;
+            const unsigned long long best_seen =
+                __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t stop_seen = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool hit = false;
+            for (; q != 0; --q, i0 += (uint64_t)kWaveBlock) {
+                const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, kc, i0, lane, loff);
+                if (g != kNoHitG) {
+                    best = g < best ? g : best;
+                    hit = true;
+                    break;
+                }
+            }
+            best = best_seen < best ? best_seen : best;
+            stop = stop_seen;
+            if (hit || left == 0 || stop != 0u || global_of_local(i0, L.rbits, L.base_tb) >= best) break;
+        }
+#else
         // Issued now, consumed at the next claim: the latency hides behind the chunk.
         const unsigned long long best_next =
             __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -598,6 +634,7 @@ md5_search_kernel(const Launch L) {
         }
         best = best_next < best ? best_next : best;
         stop = stop_next;
+#endif
         claim = next;
     }
     // Retirement is counted per workgroup (a quarter of the atomics on the

@@ -297,6 +297,20 @@ int dpow_plan_candidate(const uint8_t *nonce, size_t nonce_len, uint32_t worker_
     return 0;
 }
 
+int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint64_t k, uint32_t iv_d,
+                         uint32_t state_d) {
+    std::vector<PlannedLaunch> plan;
+    const int n = plan_window(nonce, nonce_len, ntz, 0, 0, k, k + 1, plan);
+    if (n != 1) return set_error(n < 0 ? n : DPOW_EINVAL, "dpow_diag_dword_test: bad arguments");
+    const Launch &L = plan[0].L;
+    const uint32_t nblk = plan[0].info.nblk;
+    // one final block: the chaining value is the planner's (midstate or RFC IV)
+    if (nblk == 1 && iv_d != L.iv[3]) return set_error(DPOW_EINVAL, "dpow_diag_dword_test: iv_d != iv[3]");
+    const uint32_t D = iv_d + state_d;
+    const bool pre = use_d_equality(nblk, ntz) ? state_d == L.deq : D <= L.dle;
+    return pre && (D & L.dmask) == 0u ? 1 : 0;
+}
+
 int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
                 uint32_t worker_bits, uint64_t k_begin, uint64_t k_end, uint64_t *best_global_idx,
                 uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len) {

@@ -100,6 +100,8 @@ def lib():
         "dpow_device_count": (ctypes.c_int, []),
         "dpow_diag_valu_rate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(ctypes.c_double)]),
+        "dpow_diag_dword_test": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64,
+                                                ctypes.c_uint32, ctypes.c_uint32]),
         "dpow_worker_new": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
         "dpow_worker_free": (None, [vp]),
         "dpow_worker_mine": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,

@@ -25,7 +25,9 @@ extern "C" {
  *        26/27 kind 22's pattern on fixed registers whose operands sit in distinct / the
  *        same VGPR bank (register index mod 4), 28 v_mad_u32_u24, 29 v_dot2_u32_u16,
  *        30 v_bitop3_b16, 31 v_lshlrev_b64, 32 v_lshl_add_u64, 33 v_pk_mov_b32 (31-33 count
- *        one instruction per register pair).
+ *        one instruction per register pair), 34 v_add_u32_sdwa (src1 WORD_1), 35 v_add_u16_sdwa
+ *        (dst WORD_1, low half preserved), 36 the kernel's order-2 step pair with a 16-bit
+ *        rotate, 37 the same with each rotate + add as two SDWA adds.
  * *lane_ops_per_s = wave64 instructions x 64 / s; *clock_ghz = mean in-kernel
  * shader clock (s_memtime / s_memrealtime).  Returns 0, or < 0 on error. */
 int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *clock_ghz);
@@ -36,6 +38,17 @@ int dpow_diag_valu_rate(int device, int kind, double *lane_ops_per_s, double *cl
  *   mode 2: a 16-byte device->host hipMemcpyAsync + hipStreamSynchronize.
  * The floor under time-to-secret at small N.  Returns 0, or < 0 on error. */
 int dpow_diag_launch_latency(int device, int mode, int reps, double *median_us);
+
+/* The hash loop's per-candidate D-word test (md5_search_kernel.h hash_wave_block), on
+ * the host, with the launch fields the planner derives for (nonce, ntz) at chunk index
+ * k: the one-compare prefilter (state word == -iv[3] for the D-equality kernels, else
+ * D <= dle) and the rare path's exact nibble mask.  `state_d` is the last block's raw D
+ * state word, D = iv_d + state_d, where iv_d is the chaining value entering that block
+ * (for two final blocks the first block's output, per candidate, so the caller passes
+ * it).  Returns 1 if the candidate reaches the hit path (for ntz > 8 still subject to
+ * the full-digest check), 0 if not, < 0 on error. */
+int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint64_t k,
+                         uint32_t iv_d, uint32_t state_d);
 
 #ifdef __cplusplus
 }

@@ -16,12 +16,13 @@
 // the first hit of a wave-block (lowest slot, then lowest lane) goes to
 // atomicMin on the global index g = k * 256 + threadByte, which is monotone in
 // i, so the minimum is the reference's first hit.  A wave stops at the first
-// chunk whose first index is >= the current minimum, so every candidate below
-// the answer is evaluated and the result is deterministic.
+// chunk, or group of DPOW_POLL_WB wave-blocks within one, whose first index is
+// >= the current minimum, so every candidate below the answer is evaluated and
+// the result is deterministic.
 //
 // Workgroup 0 of the grid is a watcher: one lane polls the pinned host cancel
 // flag (Found/Cancel, worker.go:194,209) and raises Ctrl::stop, which every
-// worker wave reads once per chunk together with Ctrl::best.  The workgroup that
+// worker wave reads every DPOW_POLL_WB wave-blocks together with Ctrl::best.  The workgroup that
 // retires last writes the launch's completion record (Snap) to pinned host
 // memory, which the host polls.
 #pragma once
@@ -584,8 +585,8 @@ md5_search_kernel(const Launch L) {
         const uint64_t b_begin = claim * L.chunk;
         const uint32_t nb = (uint32_t)(b_begin + L.chunk < L.n_wblocks ? L.chunk : L.n_wblocks - b_begin);
         const uint64_t i_first = L.wb_begin + b_begin * (uint64_t)kWaveBlock;
-        // Early exit at chunk granularity (<= 32 wave-blocks): stop on a cancel,
-        // or once this chunk starts at or above the best index found so far.
+        // Early exit at a claim: stop on a cancel, or once this chunk starts at
+        // or above the best index found so far.
         // Everything below the best has been or is being hashed by earlier claims.
         if (stop != 0u ||
             global_of_local(i_first < L.i_begin ? L.i_begin : i_first, L.rbits, L.base_tb) >= best)

@@ -314,9 +314,19 @@ def cpu_baseline(threads, seconds):
     rate = hashes / secs
     k_count = max(1, int(rate * seconds / (R * W)))
     secs, hashes = o.cpu_bench(NONCE, SWEEP_NTZ, W, K0, k_count)
+    # Time-to-secret of BASELINE configs 1 and 2 on one core (the reference's one miner
+    # goroutine per task), next to the GPU's time_to_secret for the same (nonce, N).
+    tts = {}
+    for ntz in (3, 6):
+        t = time.perf_counter()
+        hit = o.mine_window(NONCE, ntz, 0, 0, 0, 1 << 20)
+        ms = (time.perf_counter() - t) * 1e3
+        assert hit is not None
+        tts[f"{bytes(NONCE).hex()}/{ntz}"] = {"ms": round(ms, 3), "global_idx": hit[1], "cores": 1}
     return {"value": round(hashes / secs / 1e9, 6), "unit": "GH/s", "cores": W, "kind": "port",
             "sample": f"{hashes} candidates (k in [2^24, 2^24+{k_count}) x {W} workers, nonce [1,2,3,4], "
-                      f"N=32) in {secs:.2f} s; C restatement of worker.go:318-400 (oracle/dpow_oracle.c)"}
+                      f"N=32) in {secs:.2f} s; C restatement of worker.go:318-400 (oracle/dpow_oracle.c)",
+            "time_to_secret": tts}
 
 
 if __name__ == "__main__":

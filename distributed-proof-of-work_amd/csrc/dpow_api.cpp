@@ -62,6 +62,10 @@ constexpr uint64_t kBlocksPerCu = 8;
 constexpr uint64_t kClaimsPerWave = 16;
 constexpr uint64_t kMinChunk = 4;
 constexpr uint64_t kMaxChunk = DPOW_MAX_CHUNK;
+#ifndef DPOW_TAIL_CLAIMS
+#define DPOW_TAIL_CLAIMS 2  // small claims per wave at the end of a launch (0: none; A/B switch)
+#endif
+constexpr uint64_t kTailClaimsPerWave = DPOW_TAIL_CLAIMS;
 // Claim-counter slots (kClaimSlot counters each) used round-robin by the launches
 // of a search: zeroed at search start, re-zeroed by each launch's last workgroup.
 constexpr size_t kClaimRing = 64;
@@ -377,7 +381,13 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
         if (chunk < kMinChunk) chunk = kMinChunk;
         if (chunk > kMaxChunk) chunk = kMaxChunk;
-        const uint64_t n_chunks = (L.n_wblocks + chunk - 1) / chunk;
+        // Guided tail: the last ~kTailClaimsPerWave claims per wave are
+        // kMinChunk wave-blocks, so the waves of a launch run dry together.
+        const uint64_t chunk_tail = kMinChunk < chunk ? kMinChunk : chunk;
+        const uint64_t tail_wb = worker_blocks * wpb * kTailClaimsPerWave * chunk_tail;
+        const uint64_t n_big = L.n_wblocks > tail_wb ? (L.n_wblocks - tail_wb) / chunk : 0;
+        const uint64_t rest = L.n_wblocks - n_big * chunk;
+        const uint64_t n_chunks = n_big + (rest + chunk_tail - 1) / chunk_tail;
         // No more waves than chunks, but a worker block for every counter that
         // holds a chunk (block b serves counter (b - 1) % kClaimCounters).
         uint64_t need_blocks = (n_chunks + wpb - 1) / wpb;
@@ -388,6 +398,8 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
             return set_error(DPOW_EINVAL, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.chunk = (uint32_t)chunk;
+        L.chunk_tail = (uint32_t)chunk_tail;
+        L.n_big = n_big;
         L.n_chunks = n_chunks;
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
         L.done_target = done_target;

@@ -96,8 +96,10 @@ struct Launch {
     uint32_t deq;          // D-equality kernels (one final block, ntz >= 8): D == 0 <=> state word == deq = -iv[3]
     uint32_t ntz;          // requested trailing zeros (full digest check when > 8)
     uint32_t done_target;  // Ctrl::done once this launch's worker workgroups have retired
-    uint32_t chunk;        // wave-blocks per claim
-    uint64_t n_chunks;     // claims covering n_wblocks
+    uint32_t chunk;        // wave-blocks per claim of the first n_big claims
+    uint32_t chunk_tail;   // wave-blocks per claim after them (the launch's tail: small claims)
+    uint64_t n_big;        // claims of `chunk` wave-blocks
+    uint64_t n_chunks;     // claims covering n_wblocks (n_big + tail claims)
     unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;

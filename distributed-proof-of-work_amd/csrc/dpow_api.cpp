@@ -58,7 +58,10 @@ int hip_fail(hipError_t e, const char *what) {
 // claims/us (MI355X_MICROARCH.md "dequeue") and a wave hashes one wave-block
 // in ~6 us, so 8k waves at chunk c ask ~1300/c claims/us of the 8 counters.
 // Small launches get fewer workgroups instead of smaller chunks.
-constexpr uint64_t kBlocksPerCu = 8;
+#ifndef DPOW_BLOCKS_PER_CU
+#define DPOW_BLOCKS_PER_CU 8
+#endif
+constexpr uint64_t kBlocksPerCu = DPOW_BLOCKS_PER_CU;
 constexpr uint64_t kClaimsPerWave = 16;
 constexpr uint64_t kMinChunk = 4;
 constexpr uint64_t kMaxChunk = DPOW_MAX_CHUNK;

@@ -55,7 +55,22 @@ namespace dpow {
 #ifndef DPOW_POLL_WB
 #define DPOW_POLL_WB 16
 #endif
+// Tail priority (see the claim loop): profiles/r01_ab_tail_prio.log, sweep windows at
+// workerBits 3 (2^29-candidate launches) 209.5 -> 212.8 GH/s, workerBits 0 217.4 -> 218.3.
+#ifndef DPOW_TAIL_PRIO
+#define DPOW_TAIL_PRIO 1
+#endif
 constexpr uint32_t kPollWb = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 1;
+// Diagnostic builds only (tools/wave_trace.py): every worker wave records
+// {start, first claim, exit} in s_memrealtime ticks (100 MHz) and its hashed
+// wave-blocks, read back with dpow_diag_wave_trace.
+#ifndef DPOW_WAVE_TRACE
+#define DPOW_WAVE_TRACE 0
+#endif
+#if DPOW_WAVE_TRACE
+constexpr uint32_t kTraceWaves = 8192;
+static __device__ unsigned long long g_wave_trace[kTraceWaves * 4];
+#endif
 
 template <int I>
 DPOW_DEV uint32_t md5_fn(uint32_t x, uint32_t y, uint32_t z) {
@@ -542,6 +557,10 @@ md5_search_kernel(const Launch L) {
         watcher(L);
         return;
     }
+#if DPOW_WAVE_TRACE
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_first = 0, n_wb = 0;
+#endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t loff = lane_offset(L.rbits, lane);
     KConst kc;
@@ -560,9 +579,19 @@ md5_search_kernel(const Launch L) {
     // least min(n_chunks, 8) worker blocks, so every counter holding a chunk
     // has waves.  Workgroups go round-robin to XCDs, so each counter's waves
     // share one XCD.
+#if DPOW_TAIL_PRIO
+    // Older waves win the SIMD's issue arbitration, so the youngest waves of a
+    // CU barely progress until the launch drains, and then finish chunks they
+    // claimed early.  Every worker wave runs at priority 1 and drops to 0 once
+    // it holds a tail claim: the waves still on earlier chunks issue first.
+    __builtin_amdgcn_s_setprio(1);
+#endif
     uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
     uint64_t claim = skip ? L.n_chunks : claim_next(L.claim + x * kClaimStride, x, lane);
+#if DPOW_WAVE_TRACE
+    t_first = __builtin_amdgcn_s_memrealtime() + (claim & 0);
+#endif
     uint32_t hops = 0;
     for (;;) {
 #if DPOW_STEAL
@@ -586,6 +615,9 @@ md5_search_kernel(const Launch L) {
         // launch ends on small claims, so its waves run dry within a few
         // wave-blocks of each other (the tail of a 2.5 ms launch was ~3 %).
         const bool big = claim < L.n_big;
+#if DPOW_TAIL_PRIO
+        if (!big) __builtin_amdgcn_s_setprio(0);
+#endif
         const uint64_t b_begin = big ? claim * L.chunk : L.n_big * L.chunk + (claim - L.n_big) * L.chunk_tail;
         const uint32_t csz = big ? L.chunk : L.chunk_tail;
         const uint32_t nb = (uint32_t)(b_begin + csz < L.n_wblocks ? csz : L.n_wblocks - b_begin);
@@ -613,6 +645,9 @@ md5_search_kernel(const Launch L) {
             const uint32_t stop_seen = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             bool hit = false;
             for (; q != 0; --q, i0 += (uint64_t)kWaveBlock) {
+#if DPOW_WAVE_TRACE
+                ++n_wb;
+#endif
                 const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, kc, i0, lane, loff);
                 if (g != kNoHitG) {
                     best = g < best ? g : best;
@@ -649,6 +684,15 @@ md5_search_kernel(const Launch L) {
     // operations, with no agent-scope L2 writeback); the barrier then covers
     // all four waves.  The workgroup whose count completes the launch
     // publishes its completion record.
+#if DPOW_WAVE_TRACE
+    const uint32_t wave = (blockIdx.x - 1u) * (kBlockThreads / 64) + threadIdx.x / 64u;
+    if (lane == 0 && wave < kTraceWaves) {
+        g_wave_trace[4 * wave + 0] = t_start;
+        g_wave_trace[4 * wave + 1] = t_first;
+        g_wave_trace[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
+        g_wave_trace[4 * wave + 3] = n_wb;
+    }
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -58,3 +58,13 @@ hipError_t DPOW_NAME(variant_occupancy_, DPOW_VNBLK, DPOW_VSH)(int w0, int *bloc
 }
 
 }  // namespace dpow
+
+#if DPOW_WAVE_TRACE && DPOW_VNBLK == 1 && DPOW_VSH == 0
+// Diagnostic builds only: the per-wave trace of the last one-block, SH = 0 launch.
+extern "C" int dpow_diag_wave_trace(unsigned long long *out, size_t n) {
+    if (n > dpow::kTraceWaves * 4) n = dpow::kTraceWaves * 4;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(dpow::g_wave_trace), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
+#endif

@@ -51,15 +51,20 @@ int hip_fail(hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_fail(e_, #call); \
     } while (0)
 
-// Persistent grid: one round of resident workgroups (8 four-wave workgroups per
-// CU at <= 80 SGPRs), work handed out by in-order chunk claims from 8 per-XCD
-// counters.  A chunk is sized for >= 16 claims per wave (small tail) and
-// within [kMinChunk, kMaxChunk] wave-blocks: a contended counter serves < 90
-// claims/us (MI355X_MICROARCH.md "dequeue") and a wave hashes one wave-block
-// in ~6 us, so 8k waves at chunk c ask ~1300/c claims/us of the 8 counters.
-// Small launches get fewer workgroups instead of smaller chunks.
+// Persistent grid: one round of resident workgroups (6 four-wave workgroups per
+// CU; the kernel's <= 80 SGPRs would admit 8), work handed out by in-order
+// chunk claims from 8 per-XCD counters.  A chunk is sized for >= 16 claims per
+// wave (small tail) and within [kMinChunk, kMaxChunk] wave-blocks: a contended
+// counter serves < 90 claims/us (MI355X_MICROARCH.md "dequeue") and a wave
+// hashes one wave-block in ~6 us, so 8k waves at chunk c ask ~1300/c claims/us
+// of the 8 counters.  Small launches get fewer workgroups instead of smaller
+// chunks.  Why 6, not 8: the SIMD issues oldest-first, and the five oldest
+// waves of a SIMD already take ~all its VALU cycles (tools/wave_trace.py); the
+// youngest ones hash ~1/60 of the mean and sit on the early chunks they
+// claimed, which a first hit has to wait for.  6 vs 8 (profiles/r01_ab_tail_prio.log):
+// throughput equal in every layout, time-to-secret N = 7 1.49 -> 1.37 ms.
 #ifndef DPOW_BLOCKS_PER_CU
-#define DPOW_BLOCKS_PER_CU 8
+#define DPOW_BLOCKS_PER_CU 6
 #endif
 constexpr uint64_t kBlocksPerCu = DPOW_BLOCKS_PER_CU;
 constexpr uint64_t kClaimsPerWave = 16;

@@ -7,7 +7,7 @@ sys.path.insert(0, "distributed-proof-of-work_amd")
 import distpow
 from distpow import _lib
 
-W = 8192
+W = 6144  # worker waves of a full grid (6 four-wave workgroups per CU x 256 CUs)
 lib = ctypes.CDLL(_lib.LIB_PATH)
 m = distpow.Miner(0)
 m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 24))  # warm the clock

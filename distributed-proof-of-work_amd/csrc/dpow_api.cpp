@@ -409,6 +409,7 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         L.chunk_tail = (uint32_t)chunk_tail;
         L.n_big = n_big;
         L.n_chunks = n_chunks;
+        L.n_head = 2 * worker_blocks * wpb;
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;

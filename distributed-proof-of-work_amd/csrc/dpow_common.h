@@ -100,6 +100,7 @@ struct Launch {
     uint32_t chunk_tail;   // wave-blocks per claim after them (the launch's tail: small claims)
     uint64_t n_big;        // claims of `chunk` wave-blocks
     uint64_t n_chunks;     // claims covering n_wblocks (n_big + tail claims)
+    uint64_t n_head;       // the claims every wave takes at its start (2 per wave): hashed at raised priority
     unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;

@@ -60,6 +60,9 @@ namespace dpow {
 #ifndef DPOW_TAIL_PRIO
 #define DPOW_TAIL_PRIO 1
 #endif
+#ifndef DPOW_HEAD_PRIO
+#define DPOW_HEAD_PRIO 0  // A/B switch (needs DPOW_TAIL_PRIO)
+#endif
 constexpr uint32_t kPollWb = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 1;
 // Diagnostic builds only (tools/wave_trace.py): every worker wave records
 // {start, first claim, exit} in s_memrealtime ticks (100 MHz) and its hashed
@@ -584,7 +587,11 @@ md5_search_kernel(const Launch L) {
     // CU barely progress until the launch drains, and then finish chunks they
     // claimed early.  Every worker wave runs at priority 1 and drops to 0 once
     // it holds a tail claim: the waves still on earlier chunks issue first.
+#if DPOW_HEAD_PRIO
+    __builtin_amdgcn_s_setprio(2);
+#else
     __builtin_amdgcn_s_setprio(1);
+#endif
 #endif
     uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
@@ -616,7 +623,15 @@ md5_search_kernel(const Launch L) {
         // wave-blocks of each other (the tail of a 2.5 ms launch was ~3 %).
         const bool big = claim < L.n_big;
 #if DPOW_TAIL_PRIO
+#if DPOW_HEAD_PRIO
+        // Head priority: the two claims every wave takes at its start are the
+        // launch's lowest chunks; a young wave hashes them at priority 2, so a
+        // first hit beyond them does not wait for the launch to drain.
         if (!big) __builtin_amdgcn_s_setprio(0);
+        else if (claim >= L.n_head) __builtin_amdgcn_s_setprio(1);
+#else
+        if (!big) __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
         const uint64_t b_begin = big ? claim * L.chunk : L.n_big * L.chunk + (claim - L.n_big) * L.chunk_tail;
         const uint32_t csz = big ? L.chunk : L.chunk_tail;

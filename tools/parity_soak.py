@@ -6,7 +6,8 @@
 Random nonce lengths (0..130, every kernel layout), partitions (workerBits 0..10),
 windows (every chunk-length segment, straddling segment / 2^24 boundaries) and
 trailing-zero counts (1..5); every GPU answer must equal the oracle's first hit
-(or "no hit").  Prints one JSON line with the case count.  GPU box only.
+(or "no hit").  Prints one JSON line with the case count (progress on stderr every
+30 s).  GPU box only.
 """
 import json
 import os
@@ -27,6 +28,7 @@ rnd = random.Random(seed)
 o = Oracle()
 n_cases = hits = 0
 t_end = time.time() + secs
+t_log = time.time() + 30
 with distpow.Miner(0) as m:
     while time.time() < t_end:
         nlen = rnd.randrange(131)
@@ -52,4 +54,7 @@ with distpow.Miner(0) as m:
             assert r.status == distpow.FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1]), (case, r, exp)
             hits += 1
         n_cases += 1
+        if time.time() >= t_log:  # progress line: a silent run looks hung to the GPU harness
+            print(f"... {n_cases} cases, {hits} hits", file=sys.stderr, flush=True)
+            t_log += 30
 print(json.dumps({"cases": n_cases, "hits": hits, "seed": seed, "seconds": secs}))

@@ -83,6 +83,8 @@ constexpr size_t kClaimRing = 64;
 constexpr size_t kDepth = 3;
 static_assert(kDepth < kClaimRing, "a claim slot is reused only after its launch completed");
 constexpr size_t kRing = 8;  // completion records and event pairs, indexed by launch seq (>= kDepth + 1)
+// Word of the pinned cancel page holding the stale launch sequence (Launch::stale).
+constexpr size_t kStaleWord = 8;
 // Completion-record wait: spin this long (time-to-secret), then poll at kPollNs.
 constexpr int64_t kSpinNs = 200000;
 constexpr long kPollNs = 20000;
@@ -105,7 +107,7 @@ struct dpow_ctx {
     unsigned long long *d_claims = nullptr;  // kClaimRing slots of kClaimSlot claim counters
     Snap *h_snap = nullptr;        // kRing completion records: pinned, host-coherent, mapped
     Snap *d_snap = nullptr;        // device alias
-    uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped
+    uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped: [0] the cancel flag, [kStaleWord] stale seq
     uint32_t *d_cancel = nullptr;  // device alias
     uint32_t cus = 0;
     uint64_t seq = 0;  // launches ever queued on this context (record/slot index = seq % kRing)
@@ -414,6 +416,7 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;
         L.cancel = c->d_cancel;
+        L.stale = c->d_cancel + kStaleWord;
         L.snap = c->d_snap + seq % kRing;
         L.seq = (uint32_t)(seq + 1);
         DPOW_HIP(hipEventRecord(slot.start, c->stream));
@@ -431,6 +434,12 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         const int r = consume(consumed);
         if (r < 0) return r;
         status = r;
+    }
+    if (status == DPOW_CANCELLED && consumed < launched) {
+        // Up to kDepth launches are still queued.  Mark them stale so their
+        // watchers stop them even when the caller clears the cancel flag for
+        // the context's next task before they start.
+        __atomic_store_n(&c->h_cancel[kStaleWord], (uint32_t)c->seq, __ATOMIC_RELEASE);
     }
 
     if (status == DPOW_FOUND) {

@@ -105,6 +105,7 @@ struct Launch {
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;
     const uint32_t *cancel;  // device-visible alias of the pinned host cancel flag
+    const uint32_t *stale;   // pinned: launches with seq <= *stale (mod 2^32) belong to a cancelled search
     Snap *snap;              // device alias of this launch's pinned completion record
     uint32_t seq;            // value the last workgroup writes to snap->seq
 };

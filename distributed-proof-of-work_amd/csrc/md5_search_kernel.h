@@ -469,13 +469,18 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 }
 
 // Workgroup 0, one lane: relays the host cancel flag to Ctrl::stop while the
-// launch runs; exits once every worker workgroup has retired.
+// launch runs; exits once every worker workgroup has retired.  A launch that
+// was still queued when its search returned CANCELLED stops too, even after
+// the caller cleared the flag for its next task: the host marks every launch
+// up to the last one it queued as stale (int32 sequence distance).
 DPOW_DEV void watcher(const Launch &L) {
     if (threadIdx.x != 0) return;
     for (;;) {
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (done >= L.done_target) return;
-        if (__hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (__hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+            (int32_t)(stale - L.seq) >= 0) {
             __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
@@ -545,7 +550,14 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
             }
             if (m != 0) {
                 const uint64_t g = global_of_local(ij + (uint64_t)__builtin_ctzll(m), L.rbits, L.base_tb);
-                if (lane == 0) atomicMin(&L.ctrl->best, (unsigned long long)g);
+                if (lane == 0) {
+                    // A returning atomic whose result is consumed: the wave waits (vmcnt)
+                    // until the min is performed, before its retirement barrier and the
+                    // Ctrl::done increment that lets publish() read Ctrl::best.
+                    const unsigned long long prev = __hip_atomic_fetch_min(
+                        &L.ctrl->best, (unsigned long long)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("; dpow: atomicMin performed (%0)" ::"v"(prev));
+                }
                 return g;
             }
         }
@@ -694,11 +706,12 @@ md5_search_kernel(const Launch L) {
         claim = next;
     }
     // Retirement is counted per workgroup (a quarter of the atomics on the
-    // shared counter).  Each wave's atomicMin is performed first (the
-    // workgroup-scope release waits on the wave's outstanding memory
-    // operations, with no agent-scope L2 writeback); the barrier then covers
-    // all four waves.  The workgroup whose count completes the launch
-    // publishes its completion record.
+    // shared counter).  Each wave's atomicMin has been performed already (the
+    // hit path consumes the returning atomic's result, which waits on vmcnt);
+    // the barrier then covers all four waves, so the Ctrl::done increment --
+    // and publish(), which reads Ctrl::best -- come after every hit of the
+    // workgroup.  The workgroup whose count completes the launch publishes its
+    // completion record.
 #if DPOW_WAVE_TRACE
     const uint32_t wave = (blockIdx.x - 1u) * (kBlockThreads / 64) + threadIdx.x / 64u;
     if (lane == 0 && wave < kTraceWaves) {

@@ -47,6 +47,16 @@ std::string json_bytes(const std::vector<uint8_t> &b) {
     return s + "]";
 }
 
+std::string json_escape(const std::string &in) {
+    std::string s;
+    for (char ch : in) {
+        if (ch == '"' || ch == '\\') s += '\\';
+        if ((unsigned char)ch < 0x20) continue;
+        s += ch;
+    }
+    return s;
+}
+
 // worker.go:508-510 generateWorkerTaskKey
 std::string task_key(const std::vector<uint8_t> &nonce, uint32_t ntz, uint32_t wb) {
     return hex(nonce) + "|" + std::to_string(ntz) + "|" + std::to_string(wb);
@@ -126,9 +136,10 @@ struct dpow_worker {
 
     // -- resultChan <- ----------------------------------------------------------
     void send(const std::vector<uint8_t> &nonce, uint32_t ntz, uint32_t wb, const std::vector<uint8_t> *secret,
-              uint64_t token) {
+              uint64_t token, int32_t error = 0) {
         dpow_worker_result r;
         memset(&r, 0, sizeof r);
+        r.error = error;
         r.num_trailing_zeros = ntz;
         r.worker_byte = wb;
         r.token = token;
@@ -200,8 +211,8 @@ struct dpow_worker {
             }
         }
         dpow_ctx *c = nullptr;
-        if (dpow_open(device, &c) != 0) return nullptr;
-        return c;
+        const int rc = dpow_open(device, &c);
+        return rc == 0 ? c : nullptr;
     }
     void release_ctx(dpow_ctx *c) {
         *dpow_cancel_flag(c) = 0u;
@@ -241,15 +252,29 @@ struct dpow_worker {
             k = ke;
             if (window < (1ull << 24)) window <<= 4;
         }
-        if (status < 0 || !ctx) {
-            record(t.token, "MinerError", "\"Error\":\"" + std::string(dpow_last_error()) + "\"");
-            fprintf(stderr, "dpow worker: search failed: %s\n", dpow_last_error());
-        }
         if (ctx) {
             std::lock_guard<std::mutex> g(t.m);
             t.ctx = nullptr;
         }
         if (ctx) release_ctx(ctx);
+        if (status < 0 || !ctx) {
+            // The GPU search failed (no device, a HIP error, a hit that failed host
+            // verification).  The Go miner cannot fail here; waiting for a kill
+            // would hang the coordinator until its timeout.  Report the error on
+            // the result channel and end the task.
+            const int32_t code = ctx ? status : DPOW_EHIP;
+            const std::string err = dpow_last_error();
+            record(t.token, "MinerError", fields(t.nonce, t.ntz, nullptr, &wb) + ",\"Code\":" +
+                                              std::to_string(code) + ",\"Error\":\"" + json_escape(err) + "\"");
+            fprintf(stderr, "dpow worker: search failed (%d): %s\n", code, err.c_str());
+            {
+                std::lock_guard<std::mutex> g(tasks_mu);
+                auto it = tasks.find(task_key(t.nonce, t.ntz, t.wb));
+                if (it != tasks.end() && it->second == tp) tasks.erase(it);
+            }
+            send(t.nonce, t.ntz, wb, nullptr, t.token, code);
+            return;
+        }
         if (status == DPOW_FOUND) {  // worker.go:356-396
             record(t.token, "WorkerResult", fields(t.nonce, t.ntz, &secret, &wb));
             send(t.nonce, t.ntz, wb, &secret, t.token);
@@ -259,8 +284,8 @@ struct dpow_worker {
             return;
         }
         // Killed while searching (worker.go:320-342).  A window exhausted up to
-        // DPOW_K_LIMIT or a failed search waits for the kill like the
-        // reference's never-ending loop would.
+        // DPOW_K_LIMIT waits for the kill like the reference's never-ending
+        // loop would.
         wait_kill(t);
         record(t.token, "WorkerCancel", fields(t.nonce, t.ntz, nullptr, &wb));
         send(t.nonce, t.ntz, wb, nullptr, t.token);

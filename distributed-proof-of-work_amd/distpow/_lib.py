@@ -5,11 +5,22 @@ loudly (ImportError/OSError) when the library is missing; GPU entry points fail
 with DpowError when no HIP device is visible.
 """
 import ctypes
+import fcntl
+import glob
+import hashlib
 import os
+import re
+import shutil
+import subprocess
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# DPOW_LIB_PATH overrides the in-tree library (A/B builds in tools/ab_variants.py only).
-LIB_PATH = os.environ.get("DPOW_LIB_PATH") or os.path.join(_HERE, "libdpow.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
+# DPOW_LIB_PATH overrides the in-tree library (A/B builds in tools/ab_variants.py only;
+# such a library is not checked against the source hash).
+LIB_OVERRIDE = os.environ.get("DPOW_LIB_PATH")
+LIB_PATH = LIB_OVERRIDE or os.path.join(_HERE, "libdpow.so")
 
 DPOW_NO_HIT = 0x7FFFFFFFFFFFFFFF
 DPOW_MAX_SECRET = 16
@@ -37,7 +48,7 @@ EPROTO, ETIMEOUT = -6, -7
 
 class WorkerResult(ctypes.Structure):
     _fields_ = [("num_trailing_zeros", ctypes.c_uint32), ("worker_byte", ctypes.c_uint32),
-                ("has_secret", ctypes.c_uint32), ("secret_len", ctypes.c_uint32),
+                ("has_secret", ctypes.c_uint32), ("secret_len", ctypes.c_uint32), ("error", ctypes.c_int32),
                 ("secret", ctypes.c_uint8 * DPOW_MAX_SECRET), ("token", ctypes.c_uint64),
                 ("nonce_len", ctypes.c_uint64), ("nonce", ctypes.c_uint8 * DPOW_MAX_NONCE)]
 
@@ -48,6 +59,64 @@ class Stats(ctypes.Structure):
 
 
 _lib = None
+
+
+def source_build_id(nc=2, extra=""):
+    """The build id the Makefile embeds (dpow_build_id) for the sources in this tree:
+    sha256 over csrc/{*.cpp,*.h,*.hip} (sorted), csrc/Makefile, include/*.h (sorted)
+    and the default build flags; first 16 hex digits."""
+    names = sorted({os.path.basename(p) for pat in ("*.cpp", "*.h", "*.hip")
+                    for p in glob.glob(os.path.join(CSRC, pat))})
+    files = [os.path.join(CSRC, n) for n in names] + [os.path.join(CSRC, "Makefile")]
+    files += [os.path.join(INCLUDE, n) for n in sorted(os.path.basename(p)
+                                                       for p in glob.glob(os.path.join(INCLUDE, "*.h")))]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(f"NC={nc} EXTRA={extra}\n".encode())
+    return h.hexdigest()[:16]
+
+
+def library_build_id(path=None):
+    """The build id stored in a libdpow.so file (read from the file, without loading it:
+    a dlopen'ed stale library could not be replaced in-process)."""
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        m = re.search(rb"dpow-build-id:([0-9a-f]{16})", f.read())
+    return m.group(1).decode() if m else None
+
+
+def _rebuild():
+    """make -C csrc under a lock (several test/bench processes may start at once)."""
+    if not (shutil.which("make") and (shutil.which("hipcc") or os.path.exists("/opt/rocm/bin/hipcc"))):
+        return False
+    jobs = str(min(16, os.cpu_count() or 8))
+    with open(os.path.join(CSRC, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        print(f"distpow: libdpow.so does not match the sources; rebuilding (make -j{jobs})",
+              file=sys.stderr, flush=True)
+        subprocess.check_call(["make", "-s", "-j", jobs, "-C", CSRC], stdout=sys.stderr)
+    return True
+
+
+def check_build():
+    """Make sure LIB_PATH was built from the sources in this tree: returns its build id.
+
+    A stale library is rebuilt when make/hipcc are available (DPOW_NO_AUTOBUILD=1 turns
+    that off) and refused otherwise, so nothing ever tests or benches an old build."""
+    want = source_build_id()
+    have = library_build_id(LIB_PATH)
+    if have == want:
+        return have
+    if os.environ.get("DPOW_NO_AUTOBUILD") != "1" and _rebuild():
+        have = library_build_id(LIB_PATH)
+        if have == want:
+            return have
+    raise ImportError(f"libdpow.so at {LIB_PATH} has build id {have!r}, but the sources in this tree hash to "
+                      f"{want!r}: rebuild it (make -C distributed-proof-of-work_amd/csrc)")
 
 
 def _preload_torch_hip():
@@ -64,9 +133,10 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"libdpow.so not built at {LIB_PATH}; run __graft_entry__.build() "
-                          f"(make -C distributed-proof-of-work_amd/csrc)")
+    if LIB_OVERRIDE is None:
+        check_build()
+    elif not os.path.exists(LIB_PATH):
+        raise ImportError(f"DPOW_LIB_PATH={LIB_PATH} does not exist")
     _preload_torch_hip()
     L = ctypes.CDLL(LIB_PATH)
     u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -97,6 +167,7 @@ def lib():
         "dpow_geometry": (ctypes.c_int, [vp, u32p, u32p, u32p]),
         "dpow_last_error": (ctypes.c_char_p, []),
         "dpow_abi_version": (ctypes.c_int, []),
+        "dpow_build_id": (ctypes.c_char_p, []),
         "dpow_device_count": (ctypes.c_int, []),
         "dpow_diag_valu_rate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(ctypes.c_double)]),
@@ -143,6 +214,11 @@ def valu_rate(device=0, kind=5):
     if code < 0:
         raise DpowError(code, "dpow_diag_valu_rate failed")
     return r.value, c.value
+
+
+def build_id():
+    """Source hash libdpow.so was built from (dpow_build_id)."""
+    return lib().dpow_build_id().decode()
 
 
 def last_error():

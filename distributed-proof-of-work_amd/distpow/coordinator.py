@@ -102,6 +102,9 @@ class Coordinator:
                 self._result(r)
 
     def _result(self, r):
+        if r.error:
+            self._record(r.token, "CoordinatorWorkerError", Nonce=list(r.nonce), NumTrailingZeros=r.num_trailing_zeros,
+                         WorkerByte=r.worker_byte, Code=r.error)
         if r.secret is not None:
             self._record(r.token, "CoordinatorWorkerResult", Nonce=list(r.nonce), NumTrailingZeros=r.num_trailing_zeros,
                          WorkerByte=r.worker_byte, Secret=list(r.secret))
@@ -116,9 +119,16 @@ class Coordinator:
 
     def _get(self, q):
         try:
-            return q.get(timeout=self.timeout_s)
+            r = q.get(timeout=self.timeout_s)
         except queue.Empty:
             raise CoordinatorProtocolError("timed out waiting for worker messages")
+        if r.error:
+            # A failed GPU search (no counterpart in the Go reference, whose miner cannot
+            # fail): surface it now rather than after timeout_s of waiting for ACKs.
+            raise CoordinatorProtocolError(
+                f"worker {r.worker_byte} search failed with code {r.error} "
+                f"(nonce {r.nonce.hex()}, {r.num_trailing_zeros} zeros)")
+        return r
 
     # -- CoordRPCHandler.Mine (coordinator.go:139-298) ---------------------------------------
     def mine(self, nonce, num_trailing_zeros: int, token: Optional[int] = None) -> bytes:
@@ -140,7 +150,11 @@ class Coordinator:
         for w, wb in zip(self.workers, self.worker_bytes):
             self._record(tok, "CoordinatorWorkerMine", Nonce=list(nonce), NumTrailingZeros=ntz, WorkerByte=wb)
             w.mine(nonce, ntz, wb, self.worker_bits, tok)
-        result = self._get(q)
+        try:
+            result = self._get(q)
+        except CoordinatorProtocolError:
+            self._abort(key, nonce, ntz)
+            raise
         if result.secret is None:
             raise CoordinatorProtocolError(
                 f"First worker result appears to be cancellation ACK, from workerByte = {result.worker_byte}")
@@ -164,6 +178,17 @@ class Coordinator:
             del self._tasks[key]
         self._record(tok, "CoordinatorSuccess", Nonce=list(nonce), NumTrailingZeros=ntz, Secret=list(result.secret))
         return result.secret
+
+    def _abort(self, key, nonce, ntz):
+        """A failed request: drop the task and stop the other workers' miners (their
+        ACKs are then dropped results).  The reference log.Fatal's instead."""
+        with self._tasks_mu:
+            self._tasks.pop(key, None)
+        for w, wb in zip(self.workers, self.worker_bytes):
+            try:
+                w.cancel(nonce, ntz, wb)
+            except Exception:  # the failed worker's task is gone already
+                pass
 
     def close(self):
         self._stop = True

@@ -15,12 +15,14 @@ from ._lib import ETIMEOUT, DpowError, WorkerResult, check, lib
 
 @dataclass
 class WorkerResultWithToken:
-    """worker.go:38-44; secret None is the nil-secret cancellation ACK."""
+    """worker.go:38-44; secret None is the nil-secret cancellation ACK.  error != 0 (a
+    negative DPOW_E* code) reports a failed GPU search: the task is over."""
     nonce: bytes
     num_trailing_zeros: int
     worker_byte: int
     secret: Optional[bytes]
     token: int
+    error: int = 0
 
 
 class Worker:
@@ -64,7 +66,8 @@ class Worker:
             return None
         check(code, "dpow_worker_next_result")
         return WorkerResultWithToken(bytes(r.nonce[:r.nonce_len]), r.num_trailing_zeros, r.worker_byte,
-                                     bytes(r.secret[:r.secret_len]) if r.has_secret else None, r.token)
+                                     bytes(r.secret[:r.secret_len]) if r.has_secret else None, r.token,
+                                     r.error)
 
     # -- introspection -------------------------------------------------------------
     def trace(self) -> List[dict]:

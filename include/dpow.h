@@ -145,6 +145,11 @@ int dpow_geometry(dpow_ctx *ctx, uint32_t *cus, uint32_t *blocks_per_cu, uint32_
 /* Thread-local description of the last error. */
 const char *dpow_last_error(void);
 int dpow_abi_version(void);
+/* Source hash the library was built from: 16 hex digits of sha256 over the
+ * kernel/host sources, the Makefile, these headers and the build flags.  The
+ * Python host (distpow/_lib.py) refuses a library whose id does not match the
+ * tree it runs in, so a stale build is never tested or benched. */
+const char *dpow_build_id(void);
 /* Number of visible HIP devices (0 when none; never an error). */
 int dpow_device_count(void);
 

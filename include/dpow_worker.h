@@ -35,12 +35,16 @@ extern "C" {
 typedef struct dpow_worker dpow_worker;
 
 /* One message of the worker's ResultChannel (WorkerResultWithToken, worker.go:38-44).
- * has_secret == 0 is the nil-secret cancellation ACK. */
+ * has_secret == 0 is the nil-secret cancellation ACK.  error != 0 (a negative
+ * DPOW_E* code) reports a search that failed on the GPU side -- a case the Go
+ * reference cannot have: the task is over, no further message follows for it,
+ * and the coordinator fails the request at once instead of waiting for ACKs. */
 typedef struct dpow_worker_result {
     uint32_t num_trailing_zeros;
     uint32_t worker_byte;
     uint32_t has_secret;
     uint32_t secret_len;
+    int32_t error;
     uint8_t secret[DPOW_MAX_SECRET];
     uint64_t token;      /* the task's trace token (opaque, passed through) */
     uint64_t nonce_len;

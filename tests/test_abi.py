@@ -66,3 +66,14 @@ def test_null_arguments_are_errors_not_crashes():
     assert L.dpow_open(0, None) == -1
     assert L.dpow_get_stats(None, None) == -1
     L.dpow_close(None)  # no-op
+
+
+def test_library_build_id_matches_sources():
+    """libdpow.so carries the source hash it was built from (dpow_build_id); the loader
+    refuses or rebuilds a stale library, so tests and bench run the current sources."""
+    import distpow
+    from distpow import _lib
+    want = _lib.source_build_id()
+    assert distpow.build_id() == want
+    assert _lib.library_build_id() == want
+    assert len(want) == 16 and int(want, 16) >= 0

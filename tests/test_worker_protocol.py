@@ -144,3 +144,33 @@ def test_partition_workers_race_and_min_rule(golden):
     finally:
         for w in ws:
             w.close()
+
+
+def test_failed_search_is_reported_not_hung():
+    """A miner whose GPU search fails (here: no HIP device) reports the error on the
+    result channel at once -- one message, the task is over -- instead of waiting
+    for a kill as if it were still searching (silent hang)."""
+    if distpow.device_count() > 0:
+        pytest.skip("needs a host without a visible GPU")
+    with Worker(0) as w:
+        t0 = time.perf_counter()
+        w.mine(N1, 5, 0, 0, token=3)
+        r = w.next_result(5000)
+        assert r is not None and r.error == distpow.EHIP and r.secret is None and r.token == 3
+        assert time.perf_counter() - t0 < 5
+        assert w.next_result(100) is None
+        assert w.active_tasks() == 0
+        acts = actions(w, 3)
+        assert acts == ["WorkerMine", "CacheMiss", "MinerError"]
+
+
+def test_coordinator_fails_fast_on_worker_error():
+    from distpow.coordinator import Coordinator, CoordinatorProtocolError
+    if distpow.device_count() > 0:
+        pytest.skip("needs a host without a visible GPU")
+    with Coordinator(2, timeout_s=600) as c:
+        t0 = time.perf_counter()
+        with pytest.raises(CoordinatorProtocolError, match="search failed"):
+            c.mine(N1, 5)
+        assert time.perf_counter() - t0 < 10
+        assert "CoordinatorWorkerError" in [t["action"] for t in c.trace()]

@@ -38,7 +38,7 @@ SWEEP_NTZ = 32
 CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 STRONG_TOTAL_PER_STEP = 1 << 38    # --strong: fixed total work per step
 K0 = 1 << 24                      # start of the L = 4 segment
-PROFILE_TAG = "r01"                # profiles/<tag>_summary.json of the current kernel
+PROFILE_TAG = "r02"                # profiles/<tag>_summary.json of the current kernel
 TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x4 up to 2^22 k
 TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first_ms: the first, cold)
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
@@ -59,7 +59,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the VALU issue-rate probe")
     ap.add_argument("--no-tts", action="store_true", help="skip the time-to-secret configs")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: every host core this process may use)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (gloo + --same-device only to rehearse the N>1 path on one GPU)")
@@ -141,6 +142,8 @@ def main():
     tts = {}
     ttsk = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8),
             ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5)]
+    # BASELINE config 5: N = 9 on fresh 4-byte nonces seeded random.Random(416)
+    ttsk += [(n, 9) for n in config5_fresh_nonces()]
     for nonce, n in ([] if args.no_tts else ttsk):
         runs = []
         for _ in range(TTS_RUNS):
@@ -186,15 +189,19 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_threads, args.cpu_seconds)
 
-    # HBM bytes per sweep launch from the committed rocprofv3 PMC passes of this kernel
-    # (FETCH_SIZE and WRITE_SIZE in separate passes, tools/profile_gpu.sh + tools/summarize_profile.py)
+    # Memory traffic per sweep launch from the committed rocprofv3 PMC passes of this kernel
+    # (FETCH_SIZE and WRITE_SIZE in separate passes, tools/profile_gpu.sh + tools/summarize_profile.py),
+    # uncorrected: the search reads no data, so these bytes are kernarg scalar loads, the claim
+    # atomics and the completion records -- not algorithmic HBM traffic (that is 0 per candidate).
     traffic, traffic_src = None, None
     prof = os.path.join(ROOT, "profiles", PROFILE_TAG + "_summary.json")
     if os.path.exists(prof):
         ps = json.load(open(prof))
         if "hbm_bytes_per_launch" in ps:
             traffic = int(ps["hbm_bytes_per_launch"])
-            traffic_src = f"profiles/{PROFILE_TAG}_summary.json (FETCH_SIZE+WRITE_SIZE per 2^32-candidate launch)"
+            traffic_src = (f"profiles/{PROFILE_TAG}_summary.json: FETCH_SIZE + WRITE_SIZE per "
+                           f"{ps.get('candidates_per_sweep_launch', 0)}-candidate launch, uncorrected; "
+                           "claim atomics + kernarg loads, no algorithmic HBM bytes")
 
     if rank == 0:
         cus, bpc, tpb = miner.geometry()
@@ -305,21 +312,58 @@ def cancel_latency(miner, reps=3, run_s=0.05):
     return round(sorted(lat)[len(lat) // 2], 3)
 
 
+def config5_fresh_nonces(count=4):
+    """BASELINE config 5 / SURVEY.md 8(d) item 5: fresh 4-byte nonces seeded random.Random(416)
+    (the same list tests/golden/gen_golden.py pins at N = 9)."""
+    import random
+    rnd = random.Random(416)
+    return [[rnd.randrange(256) for _ in range(4)] for _ in range(count)]
+
+
+def host_cores():
+    """Host cores this process may use, and how the box describes them: the CPU baseline runs
+    one thread per usable core (the affinity mask, capped by a cgroup CPU quota)."""
+    import subprocess
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        info["nproc"] = int(subprocess.check_output(["nproc"]).decode().strip())
+    except Exception:
+        info["nproc"] = None
+    usable = len(os.sched_getaffinity(0))
+    info["affinity"] = usable
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            info["cgroup_cpu_quota"] = int(quota) / int(period)
+            usable = min(usable, max(1, int(int(quota) / int(period))))
+    except Exception:
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return usable, info
+
+
 def cpu_baseline(threads, seconds):
     """The oracle's restatement of the reference Go loop (worker.go:318-400, incl. %x formatting and the
-    trailing-'0' scan) on host cores, workerBits partitioned, bounded sample of the same workload."""
+    trailing-'0' scan) on the host cores: a bounded sample of the same workload on one thread per
+    core, plus time-to-secret of BASELINE configs 1-3."""
     from _oracle import Oracle
     o = Oracle()
-    W = o.lib.oracle_bench_workers(threads)
-    R = 256 // W
+    usable, info = host_cores()
+    W = threads or usable
     # calibrate on a short window, then size the sample to ~`seconds`
-    k_cal = max(1, 20000 // R)
+    k_cal = 100
     secs, hashes = o.cpu_bench(NONCE, SWEEP_NTZ, W, K0, k_cal)
     rate = hashes / secs
-    k_count = max(1, int(rate * seconds / (R * W)))
+    k_count = max(1, int(rate * seconds / (256 * W)))
     secs, hashes = o.cpu_bench(NONCE, SWEEP_NTZ, W, K0, k_count)
     # Time-to-secret of BASELINE configs 1 and 2 on one core (the reference's one miner
-    # goroutine per task), next to the GPU's time_to_secret for the same (nonce, N).
+    # goroutine per task), next to the GPU's time_to_secret for the same (nonce, N) ...
     tts = {}
     for ntz in (3, 6):
         t = time.perf_counter()
@@ -327,10 +371,18 @@ def cpu_baseline(threads, seconds):
         ms = (time.perf_counter() - t) * 1e3
         assert hit is not None
         tts[f"{bytes(NONCE).hex()}/{ntz}"] = {"ms": round(ms, 3), "global_idx": hit[1], "cores": 1}
+    # ... and config 3 (N = 7, 231,910,083 candidates) as the reference's prefix fan-out over all
+    # cores: W workers (W = the largest power of two <= threads), each on its partition.
+    g7 = 231910082
+    s7, got, h7, w7 = o.cpu_mine(NONCE, 7, W, (g7 >> 8) + 1)
+    assert got == g7, got
+    tts[f"{bytes(NONCE).hex()}/7"] = {"ms": round(s7 * 1e3, 3), "global_idx": got, "cores": w7,
+                                      "candidates": h7, "workers": w7, "worker_bits": w7.bit_length() - 1}
     return {"value": round(hashes / secs / 1e9, 6), "unit": "GH/s", "cores": W, "kind": "port",
-            "sample": f"{hashes} candidates (k in [2^24, 2^24+{k_count}) x {W} workers, nonce [1,2,3,4], "
-                      f"N=32) in {secs:.2f} s; C restatement of worker.go:318-400 (oracle/dpow_oracle.c)",
-            "time_to_secret": tts}
+            "sample": f"{hashes} candidates (k in [2^24, 2^24+{W}x{k_count}) over {W} threads, workerBits 0 "
+                      f"each, nonce [1,2,3,4], N=32) in {secs:.2f} s; C restatement of worker.go:318-400 "
+                      f"(oracle/dpow_oracle.c)",
+            **info, "time_to_secret": tts}
 
 
 if __name__ == "__main__":

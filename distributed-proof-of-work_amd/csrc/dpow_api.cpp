@@ -15,6 +15,8 @@
 #include <string.h>
 #include <time.h>
 
+#include <atomic>
+#include <algorithm>
 #include <chrono>
 #include <mutex>
 #include <string>
@@ -88,6 +90,20 @@ constexpr size_t kStaleWord = 8;
 // Completion-record wait: spin this long (time-to-secret), then poll at kPollNs.
 constexpr int64_t kSpinNs = 200000;
 constexpr long kPollNs = 20000;
+
+// Searches in flight per device in this process.  Several logical workers may
+// share one GPU (the coordinator mirror places W workers round-robin on the
+// node's devices; BASELINE config 4 runs 8 on one in the 1-GPU bench): each
+// search then sizes its persistent grids to its share of the device, so the
+// worker holding the answer is not starved by grids that fill every CU slot.
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_active[kMaxDevices];
+
+struct ActiveSearch {
+    int dev;
+    explicit ActiveSearch(int d) : dev(d) { g_active[dev].fetch_add(1, std::memory_order_relaxed); }
+    ~ActiveSearch() { g_active[dev].fetch_sub(1, std::memory_order_relaxed); }
+};
 
 // Timing of one queued launch (its HIP events), harvested into dpow_stats
 // lazily -- never on the path between a hit and dpow_search returning.
@@ -301,8 +317,12 @@ int dpow_plan_candidate(const uint8_t *nonce, size_t nonce_len, uint32_t worker_
                         uint64_t local_idx, uint32_t iv_out[4], uint32_t words_out[32], uint32_t *nblk_out) {
     if (!iv_out || !words_out || !nblk_out) return set_error(DPOW_EINVAL, "dpow_plan_candidate: NULL argument");
     const uint64_t k = local_idx >> remainder_bits(worker_bits);
+    // The launch a search from the start of k's chunk-length segment would use
+    // (it spans the 2^24-k segments up to k: the segment-word path of the kernel).
+    const uint32_t clen = chunk_len_of(k);
+    const uint64_t k_first = (!DPOW_SPAN || clen == 0) ? k : 1ull << (8 * (clen - 1));
     std::vector<PlannedLaunch> plan;
-    int n = plan_window(nonce, nonce_len, 0, worker_byte, worker_bits, k, k + 1, plan);
+    int n = plan_window(nonce, nonce_len, 0, worker_byte, worker_bits, k_first, k + 1, plan);
     if (n != 1) return set_error(n < 0 ? n : DPOW_EINVAL, "dpow_plan_candidate: bad arguments");
     for (int w = 0; w < 4; ++w) iv_out[w] = plan[0].L.iv[w];
     memset(words_out, 0, 32 * sizeof(uint32_t));
@@ -342,7 +362,15 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     int rc = planner.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
     if (rc < 0) return set_error(rc, "dpow_search: planning failed");
     DPOW_HIP(hipSetDevice(c->device));
+    if (c->device >= kMaxDevices) return set_error(DPOW_EINVAL, "dpow_search: device ordinal too large");
+    const ActiveSearch active(c->device);
 
+    {   // keep the stale mark within 2^30 launches of the present (int32 distance in the watcher)
+        uint32_t *st = &c->h_cancel[kStaleWord];
+        const uint32_t next = (uint32_t)(c->seq + 1);
+        if ((int32_t)(next - __atomic_load_n(st, __ATOMIC_RELAXED)) > (1 << 30))
+            __atomic_store_n(st, next - (1u << 30), __ATOMIC_RELAXED);
+    }
     const uint64_t bound = *best_global_idx;
     hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot), bound, c->stream);
     if (e != hipSuccess) return hip_fail(e, "search_reset");
@@ -387,10 +415,22 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         if (harvest(c, slot) < 0) return DPOW_EHIP;  // the slot's previous launch
         Launch &L = pl.L;
         uint64_t worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
-        if (worker_blocks > (uint64_t)c->cus * kBlocksPerCu) worker_blocks = (uint64_t)c->cus * kBlocksPerCu;
+        // This search's share of the device's resident workgroups (1 / searches in flight on it).
+        const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
+        const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * kBlocksPerCu / share, kClaimCounters);
+        if (worker_blocks > max_blocks) worker_blocks = max_blocks;
         uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
         if (chunk < kMinChunk) chunk = kMinChunk;
         if (chunk > kMaxChunk) chunk = kMaxChunk;
+        if (DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) {
+            // The launch spans 2^24-k segments: a power-of-two chunk and wave-blocks
+            // counted from a multiple of chunk wave-blocks put every segment boundary
+            // (a multiple of 2^24 * R indices) on a claim boundary, big or tail, so
+            // no chunk straddles one (the kernel switches constants per chunk group).
+            while (chunk & (chunk - 1)) chunk &= chunk - 1;
+            L.wb_begin = L.i_begin & ~(chunk * (uint64_t)kWaveBlock - 1);
+            L.n_wblocks = (L.i_end - L.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
+        }
         // Guided tail: the last ~kTailClaimsPerWave claims per wave are
         // kMinChunk wave-blocks, so the waves of a launch run dry together.
         const uint64_t chunk_tail = kMinChunk < chunk ? kMinChunk : chunk;

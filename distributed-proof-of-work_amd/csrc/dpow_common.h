@@ -47,6 +47,13 @@ constexpr uint32_t kBop3G = 0xE4;  // G = z ? x : y
 constexpr uint32_t kBop3H = 0x96;  // H = x ^ y ^ z
 constexpr uint32_t kBop3I = 0x39;  // I = y ^ (x | ~z)
 
+// Launches span 2^24-k segments (plan.cpp; the kernel re-derives the constants
+// of the words holding k >> 24).  A/B switch: 0 = the host splits a window at
+// every multiple of 2^24 k, as in round 1.
+#ifndef DPOW_SPAN
+#define DPOW_SPAN 1
+#endif
+
 // Candidates per lane per wave-block (interleaved for ILP).
 #ifndef DPOW_NC
 #define DPOW_NC 2
@@ -87,7 +94,8 @@ struct Launch {
     uint32_t KT[128];      // K[s] + T[16 b + word(s)] for every step s of block b
     uint64_t i_begin;      // local index range [i_begin, i_end)
     uint64_t i_end;
-    uint64_t wb_begin;     // i_begin rounded down to 64
+    uint64_t wb_begin;     // i_begin rounded down to a wave-block (64 * kNC: a wave-block never
+                           //  straddles a 2^24-k boundary)
     uint64_t n_wblocks;    // wave-blocks covering [wb_begin, i_end)
     uint32_t rbits;        // R = 1 << rbits threadBytes per k
     uint32_t base_tb;      // uint8(worker_byte << rbits)
@@ -95,6 +103,9 @@ struct Launch {
     uint32_t dle;          // prefilter D <= dle: the even-nibble part of dmask (dmask == ~dle for even ntz)
     uint32_t deq;          // D-equality kernels (one final block, ntz >= 8): D == 0 <=> state word == deq = -iv[3]
     uint32_t ntz;          // requested trailing zeros (full digest check when > 8)
+    uint32_t seg_first;    // k_begin >> 24: the chunk bytes above the low 24 bits that T / KT hold
+                           //  (a launch spans 2^24-k segments; the kernel re-derives the K + M
+                           //  constants of the words holding them when a wave enters another one)
     uint32_t done_target;  // Ctrl::done once this launch's worker workgroups have retired
     uint32_t chunk;        // wave-blocks per claim of the first n_big claims
     uint32_t chunk_tail;   // wave-blocks per claim after them (the launch's tail: small claims)
@@ -161,6 +172,20 @@ DPOW_HD uint32_t wave_uniform_v(uint64_t i0, uint32_t rbits, uint32_t base_tb) {
     const uint64_t R = 1ull << rbits;
     return base_tb | (uint32_t)(i0 & (R - 1)) | ((uint32_t)((i0 >> rbits) & 0xFFFFFFu) << 8);
 }
+// Segment-word additions (DPOW_SPAN): a launch's template holds k >> 24 =
+// seg_first at byte p + 4 (words W0 + 1 and, for SH = 3, W0 + 2); a candidate
+// in 2^24-k segment `seg` adds (seg - seg_first) << 8 SH to that 64-bit word
+// pair.  The field never overflows its bytes within one chunk length, but the
+// sum may carry from word W0 + 1 into W0 + 2.  Shared by the kernel and the
+// host emulation (dpow_plan_candidate).
+DPOW_HD void seg_word_deltas(uint32_t t1, uint32_t t2, uint32_t seg, uint32_t seg_first, uint32_t sh,
+                             uint32_t &d1, uint32_t &d2) {
+    const uint64_t t = ((uint64_t)t2 << 32) | t1;
+    const uint64_t x = t + ((uint64_t)(seg - seg_first) << (8 * sh));
+    d1 = (uint32_t)x - t1;
+    d2 = (uint32_t)(x >> 32) - t2;
+}
+
 // Global index g = k * 256 + threadByte of a local index.
 DPOW_HD uint64_t global_of_local(uint64_t i, uint32_t rbits, uint32_t base_tb) {
     const uint64_t R = 1ull << rbits;

@@ -33,6 +33,7 @@
 namespace dpow {
 
 #define DPOW_DEV __device__ __forceinline__
+#define DPOW_DEV_CONST __host__ __device__ constexpr
 
 // SGPR budget: <= 80 allocated SGPRs admit 8 four-wave workgroups per CU
 // (8 waves per SIMD, MI355X_MICROARCH.md "Residency").  Literal K constants are
@@ -105,19 +106,36 @@ struct KConst {
     uint32_t v[128];  // [64 * BLK + I]; only the entries VgprK selects are set
 };
 
+// Segment words: the message word(s) holding the chunk bytes above k's low 24
+// bits (byte p + 4 on; k >> 24 is one byte for L = 4, two for L = 5).  They
+// are launch-uniform within a 2^24-k segment, and a launch spans segments
+// (plan.cpp), so their K + M constants are re-derived per wave when it enters
+// another segment: word W0 + 1 always, W0 + 2 when SH = 3 (the two-byte field
+// of L = 5 crosses into it).
+#if DPOW_SPAN && DPOW_POLL_WB == 0
+#error "DPOW_SPAN needs the grouped chunk loop (DPOW_POLL_WB > 0)"
+#endif
+template <int NBLK, int W0, int SH>
+DPOW_DEV_CONST bool seg_word(int m) {
+    return DPOW_SPAN && (m == W0 + 1 || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2));
+}
+
 template <int NBLK, int W0, int SH>
 struct VgprK {
     // First step of block 0 in the hand-ordered pipeline (md5_tail's kI0 for
     // the hash loop's ONLY_D call with kNC candidates).
     static constexpr int kEnd0 = NBLK == 1 ? 62 : 64;
     static constexpr int kI0 = W0 + 4 < kEnd0 ? W0 + 4 : kEnd0;
+    // Steps the hash loop runs (ONLY_D: the last block stops after step 61).
+    static constexpr bool run(int blk, int i) { return !(blk == NBLK - 1 && i >= 62); }
+    // Steps reading a segment word: always held in VGPRs (updated at segment changes).
+    static constexpr bool seg(int blk, int i) { return seg_word<NBLK, W0, SH>(16 * blk + md5_word(i)) && run(blk, i); }
     static constexpr bool eligible(int blk, int i) {
         const int m = 16 * blk + md5_word(i);
         const bool zero = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
         const bool lane = m == W0 || (SH != 0 && m == W0 + 1);
         const bool piped = blk > 0 || i >= kI0;
-        const bool run = !(blk == NBLK - 1 && i >= 62);
-        return !zero && !lane && piped && run;
+        return !zero && !lane && piped && run(blk, i) && !seg(blk, i);
     }
     static constexpr int rank(int blk, int i) {
         int r = 0;
@@ -129,14 +147,22 @@ struct VgprK {
         return r;
     }
     static constexpr int count() { return rank(NBLK, 0); }
+    static constexpr int count_seg() {
+        int r = 0;
+        for (int b = 0; b < NBLK; ++b)
+            for (int j = 0; j < 64; ++j) r += seg(b, j) ? 1 : 0;
+        return r;
+    }
     // VGPRs the layout uses without VGPR constants (-Rpass-analysis=kernel-resource-usage):
     // one block 34-39 (SH = 0) / 43-49 (SH != 0), two blocks 41-43 / 49-53; each
-    // constant costs about one more.  The caps keep every kernel at <= 64.
+    // constant costs about one more.  The caps keep every kernel at <= 64; the
+    // segment-word constants count against them first.
     static constexpr int kCap = DPOW_VGPR_K_MAX >= 0 ? DPOW_VGPR_K_MAX
                                 : NBLK == 1 ? (SH == 0 ? 24 : 14)
                                             : (SH == 0 ? 20 : 10);
     static constexpr bool use(int blk, int i) {
-        return DPOW_VGPR_K && count() >= DPOW_VGPR_K_MIN && eligible(blk, i) && rank(blk, i) < kCap;
+        return seg(blk, i) || (DPOW_VGPR_K && count() >= DPOW_VGPR_K_MIN && eligible(blk, i) &&
+                               rank(blk, i) < kCap - count_seg());
     }
 };
 
@@ -150,12 +176,36 @@ DPOW_DEV void kconst_init(KConst &kc, const Launch &L) {
     }
 }
 
+// Additions to the segment words (W0 + 1, W0 + 2) for 2^24-k segment `seg`
+// (dpow_common.h seg_word_deltas).
+template <int W0, int SH>
+DPOW_DEV void seg_deltas(const Launch &L, uint32_t seg, uint32_t &d1, uint32_t &d2) {
+    seg_word_deltas(L.T[W0 + 1], L.T[W0 + 2], seg, L.seg_first, SH, d1, d2);
+}
+
+// Re-derive the VGPR-held K + M constants of the segment words (wave-uniform,
+// once per segment change: a rare branch).
+template <int NBLK, int W0, int SH, int BLK, int I>
+DPOW_DEV void kconst_seg(KConst &kc, const Launch &L, uint32_t d1, uint32_t d2) {
+    if constexpr (BLK < NBLK) {
+        if constexpr (VgprK<NBLK, W0, SH>::seg(BLK, I)) {
+            constexpr int m = 16 * BLK + md5_word(I);
+            const uint32_t k = L.KT[64 * BLK + I] + (m == W0 + 1 ? d1 : d2);
+            asm volatile("v_mov_b32 %0, %1" : "=v"(kc.v[64 * BLK + I]) : "s"(k));
+        }
+        if constexpr (I + 1 < 64) kconst_seg<NBLK, W0, SH, BLK, I + 1>(kc, L, d1, d2);
+        else kconst_seg<NBLK, W0, SH, BLK + 1, 0>(kc, L, d1, d2);
+    }
+}
+
 // Per-candidate variable message parts.
 struct VarWords {
     uint32_t lo_s[kNC];  // wave-uniform part of V << 8*SH (word W0)
     uint32_t lo_v;       // per-lane part of V << 8*SH (the same for every slot)
     uint32_t hi[kNC];    // V >> (32 - 8*SH), added for steps reading word W0+1
-    const KConst *kc;    // launch-uniform K + M constants held in VGPRs
+    const KConst *kc;    // launch-uniform K + M constants held in VGPRs (segment words: current segment)
+    uint32_t seg_d[2];   // segment-word additions for the steps that read them from L.KT (full_check's
+                         //  steps 62-63 of the last block only; the hash loop holds them all in kc)
 };
 
 // K + M of step I of block BLK for candidate j (the message word M includes the
@@ -169,8 +219,10 @@ struct StepWord {
     static constexpr bool zero_word = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
     static constexpr bool per_lane = m == W0 || (SH != 0 && m == W0 + 1);
     static constexpr bool vgpr_k = VgprK<NBLK, W0, SH>::use(BLK, I);
+    static constexpr bool seg = seg_word<NBLK, W0, SH>(m);
     static DPOW_DEV uint32_t km(const Launch &L, const VarWords &v, int j) {
         uint32_t k = zero_word ? kMd5K[I] : vgpr_k ? v.kc->v[64 * BLK + I] : L.KT[64 * BLK + I];
+        if constexpr (seg && !vgpr_k) k += v.seg_d[m == W0 + 1 ? 0 : 1];
         if constexpr (m == W0) k = (k + v.lo_s[j]) + v.lo_v;
         if constexpr (SH != 0 && m == W0 + 1) k += v.hi[j];
         return k;
@@ -443,10 +495,11 @@ DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff) {
 // Full digest test of one lane's candidate (rare path: only when the D-word
 // test passed and ntz > 8, i.e. probability 2^-32 per candidate).
 template <int NBLK, int W0, int SH>
-DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_t loff) {
+DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_t loff, uint64_t i0) {
     VarWords v;
     v.kc = &kc;
     var_words<SH>(v, 0, vs, loff);
+    seg_deltas<W0, SH>(L, (uint32_t)((i0 >> L.rbits) >> 24), v.seg_d[0], v.seg_d[1]);
     uint32_t out[4][kNC];
     md5_tail<NBLK, W0, SH, 1>(out, L, v);
     return trailing_zero_nibbles(out[0][0], out[1][0], out[2][0], out[3][0]) >= L.ntz;
@@ -523,6 +576,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
     uint32_t vs[kNC];
     VarWords v;
     v.kc = &kc;
+    v.seg_d[0] = v.seg_d[1] = 0u;  // unused: the hash loop's segment-word steps all read kc
 #pragma unroll
     for (int j = 0; j < kNC; ++j) {
         vs[j] = wave_uniform_v(i0 + 64u * j, L.rbits, L.base_tb);
@@ -545,7 +599,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
             uint64_t m = bal[j] & lane_range_mask((int64_t)(L.i_begin - ij), (int64_t)(L.i_end - ij));
             if (!EQ && m != 0) m &= __ballot((dig[3][j] & L.dmask) == 0u);
             if (m != 0 && L.ntz > 8u) {
-                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, kc, vs[j], loff);
+                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, kc, vs[j], loff, ij);
                 m = __ballot(ok);
             }
             if (m != 0) {
@@ -580,6 +634,13 @@ md5_search_kernel(const Launch L) {
     const uint32_t loff = lane_offset(L.rbits, lane);
     KConst kc;
     kconst_init<NBLK, W0, SH, 0, 0>(kc, L);
+#if DPOW_SPAN
+    // The 2^24-k segment kc's segment-word constants belong to; kept in a VGPR
+    // (wave-uniform, read once per group): an SGPR live across the hash loop
+    // costs spill reloads inside it under the 80-SGPR budget.
+    uint32_t cur_seg_v;
+    asm("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(L.seg_first));
+#endif
 
     unsigned long long best = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t stop = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -666,6 +727,22 @@ md5_search_kernel(const Launch L) {
         uint32_t left = nb;
         for (;;) {
             uint32_t q = left < kPollWb ? left : kPollWb;
+#if DPOW_SPAN
+            // A chunk never straddles a 2^24-k segment boundary (the host aligns a
+            // spanning launch's chunks to them, dpow_api.cpp), so neither does a
+            // group; entering another segment re-derives the segment words' K + M
+            // constants.  (Splitting groups at boundaries in the kernel instead
+            // costs 4 SGPR spill reloads per wave-block: tools/isa_loop.py.)
+            {
+                const uint32_t sg = (uint32_t)((i0 >> L.rbits) >> 24);
+                if (sg != __builtin_amdgcn_readfirstlane(cur_seg_v)) {
+                    asm volatile("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(sg));
+                    uint32_t d1, d2;
+                    seg_deltas<W0, SH>(L, sg, d1, d2);
+                    kconst_seg<NBLK, W0, SH, 0, 0>(kc, L, d1, d2);
+                }
+            }
+#endif
             left -= q;
             const unsigned long long best_seen =
                 __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -3,12 +3,15 @@
 // The reference enumerates, per worker partition (worker.go:301-316),
 //   for k = 0, 1, ... (chunk_k = nextChunk^k([]), worker.go:234-244, 399)
 //     for t in 0..R-1: msg = nonce || threadByte[t] || chunk_k   (worker.go:319-353)
-// A launch covers a k-range in which the message layout is uniform:
-//   * the chunk length L is constant (segment boundaries k = 1, 2^8, 2^16, 2^24, 2^32),
-//   * for L >= 4 the bytes of k above the low 24 bits are constant (split at multiples of 2^24),
-// so the only per-candidate bytes are V = threadByte | (k mod 2^24) << 8, at byte
-// offset p = nonce_len mod 64 of the first final block.  Whole nonce-only
-// blocks before it are hashed here once (midstate).
+// A launch covers a k-range in which the chunk length L is constant (segment
+// boundaries k = 1, 2^8, 2^16, 2^24, 2^32), so the message layout is uniform.
+// The per-candidate bytes are V = threadByte | (k mod 2^24) << 8, at byte
+// offset p = nonce_len mod 64 of the first final block, and for L >= 4 the
+// bytes of k >> 24 at p + 4, which change once every 2^24 k: the template
+// holds the launch's first value (Launch::seg_first) and the kernel re-derives
+// the K + M constants of the word(s) holding them when a wave moves into
+// another 2^24-k segment.  Whole nonce-only blocks before p are hashed here
+// once (midstate).
 #include "plan.h"
 
 #include <string.h>
@@ -26,8 +29,8 @@ uint32_t chunk_len_of(uint64_t k) {
 uint64_t segment_end(uint64_t k) {
     const uint32_t L = chunk_len_of(k);
     if (L == 0) return 1;
-    if (L <= 3) return 1ull << (8 * L);
-    return ((k >> 24) + 1) << 24;
+    if (!DPOW_SPAN && L >= 4) return ((k >> 24) + 1) << 24;
+    return 1ull << (8 * L);
 }
 
 uint32_t remainder_bits(uint32_t worker_bits) { return 8u - (worker_bits % 9u); }
@@ -86,7 +89,7 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
         for (int s = 0; s < 64; ++s) Lh.KT[64 * b + s] = kMd5K[s] + Lh.T[16 * b + md5_word(s)];
     Lh.i_begin = k << rbits_;
     Lh.i_end = ke << rbits_;
-    Lh.wb_begin = Lh.i_begin & ~63ull;
+    Lh.wb_begin = Lh.i_begin & ~(uint64_t)(kWaveBlock - 1);
     Lh.n_wblocks = (Lh.i_end - Lh.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
     Lh.rbits = rbits_;
     Lh.base_tb = base_tb_;
@@ -94,6 +97,7 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     Lh.dle = tail_prefilter_le(ntz_);
     Lh.deq = 0u - iv_[3];
     Lh.ntz = ntz_;
+    Lh.seg_first = (uint32_t)(k >> 24);
     pl.info.k_begin = k;
     pl.info.k_end = ke;
     pl.info.i_begin = Lh.i_begin;
@@ -127,6 +131,13 @@ void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words
     const uint32_t sh = pl.info.sh, w0 = pl.info.w0;
     words[w0] += V << (8 * sh);
     if (sh) words[w0 + 1] += V >> (32 - 8 * sh);
+    if (DPOW_SPAN) {  // the segment words, as the kernel re-derives them (md5_search_kernel.h seg_word)
+        uint32_t d1, d2;
+        const uint32_t seg = (uint32_t)((local_idx >> Lh.rbits) >> 24);
+        seg_word_deltas(Lh.T[w0 + 1], Lh.T[w0 + 2], seg, Lh.seg_first, sh, d1, d2);
+        words[w0 + 1] += d1;
+        if (sh == 3 && w0 + 2 != 16 * pl.info.nblk - 2) words[w0 + 2] += d2;
+    }
 }
 
 }  // namespace dpow

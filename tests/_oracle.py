@@ -13,7 +13,9 @@ ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
 
 
 def build_oracle():
-    if not os.path.exists(ORACLE_SO):
+    # make is a no-op when the library is current (a stale one would lack new entry points)
+    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(
+            os.path.join(ORACLE_DIR, "dpow_oracle.c")):
         subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
     return ORACLE_SO
 
@@ -43,6 +45,10 @@ class Oracle:
         L.oracle_cpu_bench.restype = ctypes.c_double
         L.oracle_bench_workers.argtypes = [ctypes.c_uint]
         L.oracle_bench_workers.restype = ctypes.c_uint
+        L.oracle_cpu_mine.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint,
+                                      ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint)]
+        L.oracle_cpu_mine.restype = ctypes.c_double
 
     def md5(self, msg: bytes) -> bytes:
         out = (ctypes.c_uint8 * 16)()
@@ -80,6 +86,14 @@ class Oracle:
         if r == 0:
             return None
         return list(sec.raw[:slen.value]), g.value, loc.value
+
+    def cpu_mine(self, nonce, ntz, nthreads, k_end):
+        """(seconds, min global idx or None, candidates hashed, workers) of the W-worker
+        prefix fan-out on host threads (oracle_cpu_mine)."""
+        g, h, w = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint()
+        secs = self.lib.oracle_cpu_mine(bytes(nonce), len(nonce), ntz, nthreads, k_end, ctypes.byref(g),
+                                        ctypes.byref(h), ctypes.byref(w))
+        return secs, (None if g.value == (1 << 64) - 1 else g.value), h.value, w.value
 
     def cpu_bench(self, nonce, ntz, nthreads, k_begin, k_count):
         h = ctypes.c_uint64()

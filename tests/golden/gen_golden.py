@@ -15,13 +15,24 @@ outputs cannot be produced by running it.  The vectors here come from
 
 Every case is also checked against SURVEY.md Appendix A where the survey lists it.
 
-Usage:  python tests/golden/gen_golden.py [--big]
+  * --deep (added in round 2): N = 9 and 10 first hits (6.9e10 / 1.1e12
+    candidates expected), beyond the byte-wise oracle.  They come from
+    tests/golden/fast_scan.c, an AVX-512 restatement of the same enumeration,
+    which is first cross-checked against every N <= 8 golden above; each new hit
+    is then verified with hashlib and its neighbourhood (the 16 k before it) is
+    re-searched with the byte-wise C oracle.  Written to the "deep_hits" list,
+    the rest of the file is kept as it is.  Cases: BASELINE config 5's "N = 9 on
+    fresh nonces seeded random.Random(416)" (4 four-byte nonces; SURVEY.md
+    section 8(d) item 5), the config-1/2/5 nonces at N = 9, and [1,2,3,4] at N = 10.
+
+Usage:  python tests/golden/gen_golden.py [--big] | --deep
 """
 import argparse
 import ctypes
 import hashlib
 import json
 import os
+import random
 import sys
 import threading
 
@@ -168,10 +179,75 @@ def c_mine_parallel(lib, nonce, ntz, k_end, nthreads=8, span=1 << 19):
     return None
 
 
+def config5_fresh_nonces(count=4):
+    """BASELINE config 5 / SURVEY.md 8(d) item 5: fresh 4-byte nonces seeded random.Random(416)."""
+    rnd = random.Random(416)
+    return [[rnd.randrange(256) for _ in range(4)] for _ in range(count)]
+
+
+def build_fast_scan():
+    import subprocess
+    out_dir = os.path.join(HERE, "build")
+    os.makedirs(out_dir, exist_ok=True)
+    exe = os.path.join(out_dir, "fast_scan")
+    subprocess.check_call(["gcc", "-O3", "-march=native", "-pthread", "-o", exe, os.path.join(HERE, "fast_scan.c")])
+    return exe
+
+
+def fast_scan(exe, nonce, ntz, k_end=1 << 40, threads=None):
+    import subprocess
+    threads = threads or os.cpu_count() or 8
+    out = subprocess.check_output([exe, bytes(nonce).hex(), str(ntz), "0", str(k_end), str(threads)]).decode().split()
+    if out[0] == "none":
+        return None
+    g = int(out[1])
+    k = g >> 8
+    return [g & 0xFF] + chunk_of(k), g
+
+
+def deep(path):
+    """N = 9 / 10 first hits via fast_scan, cross-checked first (see module docstring)."""
+    import time
+    with open(path) as f:
+        out = json.load(f)
+    exe = build_fast_scan()
+    lib = load_oracle()
+    for e in out["first_hits"]:  # every N <= 8 golden, incl. the 4.1e9-candidate N = 8 cases
+        r = fast_scan(exe, e["nonce"], e["ntz"], k_end=(e["global_idx"] >> 8) + 2)
+        assert r is not None and (r[0], r[1]) == (e["secret"], e["global_idx"]), (e, r)
+    print("fast_scan agrees with all", len(out["first_hits"]), "first-hit goldens", file=sys.stderr)
+    cases = [(n, 9, "config5-fresh-Random(416)") for n in config5_fresh_nonces()]
+    cases += [([1, 2, 3, 4], 9, "config1/2 nonce"), ([5, 6, 7, 8], 9, "config5 nonce"),
+              ([2, 2, 2, 2], 9, "config5 nonce"), ([1, 2, 3, 4], 10, "config1/2 nonce, N=10")]
+    done = {(tuple(e["nonce"]), e["ntz"]) for e in out.get("deep_hits", [])}
+    out.setdefault("deep_hits", [])
+    for nonce, n, why in cases:
+        if (tuple(nonce), n) in done:
+            continue
+        t = time.time()
+        secret, g = fast_scan(exe, nonce, n)
+        h = md5hex(nonce, secret)
+        assert has_num_zeroes_suffix(h, n), (nonce, n, secret, h)
+        k = g >> 8
+        # the byte-wise oracle agrees on the neighbourhood: no hit in the 16 k before, this one at k
+        near = c_mine(lib, nonce, n, 0, 0, max(0, k - 16), k + 1)
+        assert near is not None and near[0] == secret and near[1] == g, (nonce, n, near, g)
+        out["deep_hits"].append({"nonce": list(nonce), "ntz": n, "secret": secret, "global_idx": g, "md5": h,
+                                 "source": "fast-scan", "case": why})
+        print(f"deep hit {nonce} N={n}: {secret} g={g} ({time.time() - t:.0f} s)", file=sys.stderr)
+        with open(path, "w") as f:  # checkpoint after every case
+            json.dump(out, f, indent=0, separators=(",", ":"))
+            f.write("\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true", help="also compute N=7/8 cases via the C oracle")
+    ap.add_argument("--deep", action="store_true", help="add N=9/10 hits (fast_scan) to the existing file")
     args = ap.parse_args()
+    if args.deep:
+        deep(os.path.join(HERE, "pow_golden.json"))
+        return
 
     out = {"rfc1321": [{"msg_hex": m.encode().hex(), "md5": d} for m, d in RFC1321_SUITE],
            "first_hits": [], "partitions": [], "windows": [], "nonce_lengths": []}

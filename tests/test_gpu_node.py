@@ -1,0 +1,95 @@
+"""The product collective path on the GPU: node_mine over the real Miner.search.
+
+Two processes (spawned, each with its own HIP runtime) play two ranks of a
+node -- both on device 0 of the one-GPU box -- with the gloo backend for the
+batch-boundary all-reduce MIN of [best index, running].  Rank r owns the
+workerBits = 1 partition r (coordinator.go:127,326); the node's answer must be
+the workerBits = 0 golden (the min rule), owned by the
+partition that holds it, and a cancel on one rank must stop both at the same
+batch (coordinator.go:210-230 -> the vote in the all-reduce).
+"""
+import os
+import socket
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, cases, out_q):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "distributed-proof-of-work_amd"))
+    import threading
+    import time
+
+    import torch  # noqa: F401  (one HIP runtime for torch and libdpow)
+    import torch.distributed as dist
+
+    import distpow
+    from distpow.node import node_mine
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    res = []
+    with distpow.Miner(0) as m:
+        search = lambda *a: m.search(*a[:6], bound=a[6])  # noqa: E731  (node_mine's search_fn)
+        for nonce, ntz in cases:
+            r = node_mine(search, nonce, ntz, rank, world, batch_k=1 << 8)
+            res.append((r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner, r.batches))
+        # a real cancel on the last rank: its pinned flag stops its kernel mid-launch, the
+        # search returns CANCELLED and the all-reduce's running slot stops every rank
+        if rank == world - 1:
+            threading.Timer(0.3, m.cancel).start()
+        t0 = time.perf_counter()
+        r = node_mine(search, [1, 2, 3, 4], 32, rank, world, batch_k=1 << 20, k_start=1 << 24,
+                      batch_k_max=1 << 24)
+        m.clear_cancel()
+        res.append((r.status, r.batches, time.perf_counter() - t0))
+    out_q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_node_mine_two_ranks_on_gpu(golden):
+    import torch.multiprocessing as mp
+
+    want = [([1, 2, 3, 4], 6), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8), ([5, 6, 7, 8], 5)]
+    exp = {(tuple(e["nonce"]), e["ntz"]): e for e in golden["first_hits"]}
+    cases = [c for c in want if (tuple(c[0]), c[1]) in exp]
+    assert len(cases) == len(want)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        outs = dict(q.get(timeout=100) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    for rank in range(world):
+        for (nonce, ntz), (status, g, secret, owner, batches) in zip(cases, outs[rank][:-1]):
+            e = exp[(tuple(nonce), ntz)]
+            assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, nonce, ntz, g)
+            assert owner == (g & 0xFF) >> 7
+        status, batches, secs = outs[rank][-1]
+        assert status == 2, outs[rank][-1]  # CANCELLED on every rank
+        assert secs < 5
+    # the ranks agree batch by batch
+    assert [r[4] for r in outs[0][:-1]] == [r[4] for r in outs[1][:-1]]
+    assert outs[0][-1][1] == outs[1][-1][1]

@@ -202,16 +202,16 @@ def test_native_cli(tmp_path):
     print("cli sweep", out)
 
 
-def test_claim_slot_recycling_many_launches(miner, oracle):
-    """A window of 80 launches (worker_bits = 8: one thread byte per k, so each
-    2^24-k launch of the L = 4 segment holds 2^24 candidates) recycles the 64
-    claim-counter slots: the whole window is hashed exactly once."""
+def test_window_spanning_80_segments(miner, oracle):
+    """A window of 80 2^24-k segments (worker_bits = 8: one thread byte per k, 2^24
+    candidates per segment) runs as one launch whose waves re-derive the segment
+    words' constants 80 times: the whole window is hashed exactly once."""
     k0 = 1 << 24
     k1 = k0 + 80 * (1 << 24)
     miner.reset_stats()
     assert miner.search([1, 2, 3, 4], 32, 77, 8, k0, k1).status == EXHAUSTED
     s = miner.stats()
-    assert s.launches == 80 and s.candidates == 80 * (1 << 24)
+    assert s.launches == 1 and s.candidates == 80 * (1 << 24)
     # A late first hit in the same partition: hashlib-valid, and the oracle
     # agrees on the 4097 candidates ending at it (no earlier hit there).
     r = miner.search([1, 2, 3, 4], 8, 77, 8, k0, k1 + 400 * (1 << 24))
@@ -300,3 +300,108 @@ def test_n8_first_hit_vs_n7_walk(miner, nlen, wbits, wb):
             break
         k = ks + 1
     assert walked >= 1
+
+
+def _all_hits(miner, nonce, ntz, wb, wbits, k0, k1, cap=2000):
+    """Every hit of a window, in order: repeated searches resuming after each hit."""
+    hits, bound_k = [], k0
+    rb = 8 - wbits % 9
+    while bound_k < k1 and len(hits) < cap:
+        r = miner.search(nonce, ntz, wb, wbits, bound_k, k1)
+        if r.status != FOUND:
+            break
+        hits.append(r.global_idx)
+        # resume at the same k for partitions with several thread bytes per k
+        k = r.global_idx >> 8
+        tbs = [((wb << rb) | j) & 255 for j in range(1 << rb)]
+        later = [t for t in tbs if t > (r.global_idx & 255)]
+        for t in later:  # the rest of this k, candidate by candidate (the window API is per k)
+            g = (k << 8) | t
+            if distpow.verify(nonce, _secret_of(g), ntz):
+                hits.append(g)
+        bound_k = k + 1
+    return hits
+
+
+@pytest.mark.parametrize("nlen,first_k,nseg", [
+    (4, (1 << 24) + 12345, 12),                # SH 0, L = 4
+    (5, (7 << 24) - 999, 10),                  # SH 1
+    (6, (200 << 24) + 1, 9),                   # SH 2
+    (7, (1 << 32) + (250 << 24) + 77, 12),     # SH 3, L = 5: k >> 24 carries from word W0+1 into W0+2
+    (8, (1 << 32) + (3 << 24) - 5, 6),         # L = 5, SH 0
+    (60, (1 << 24) + 3, 6),                    # two final blocks, W0 = 15: the segment word is block 1's word 0
+    (63, (1 << 32) + (254 << 24), 5),          # two final blocks, SH 3, L = 5: words 16 and 17
+])
+def test_spanning_launch_equals_per_segment_windows(miner, oracle, nlen, first_k, nseg):
+    """The segment-word path (DPOW_SPAN): one search over a window spanning nseg 2^24-k
+    segments from an unaligned k finds exactly the hits that searches confined to one
+    segment each find (there the template holds the segment's own k >> 24 bytes), and
+    the first one agrees with the byte-wise oracle on the 4096 k before it."""
+    rnd = random.Random(nlen)
+    nonce = [1, 2, 3, 4] if nlen == 4 else [rnd.randrange(256) for _ in range(nlen)]
+    wb, wbits, ntz = rnd.randrange(256), 8, 5  # ~16 hits per segment: every segment's constants are checked
+    k1 = first_k + nseg * (1 << 24)
+    span = _all_hits(miner, nonce, ntz, wb, wbits, first_k, k1)
+    per = []
+    k = first_k
+    while k < k1:
+        ke = min(k1, ((k >> 24) + 1) << 24)
+        per += _all_hits(miner, nonce, ntz, wb, wbits, k, ke)
+        k = ke
+    assert span == per and len(span) >= 4 * nseg, (nlen, len(span), len(per))
+    assert len({g >> 32 for g in span}) >= nseg  # hits in every segment the window covers
+    for g in span:
+        assert distpow.verify(nonce, _secret_of(g), ntz)
+    kh = span[0] >> 8
+    exp = oracle.mine_window(nonce, ntz, wb, wbits, max(first_k, kh - 4096), kh + 1)
+    assert exp is not None and exp[1] == span[0]
+
+
+def test_spanning_launch_partition_wbits3(miner):
+    """The same at workerBits 3 (32 thread bytes per k, the 8-GPU partition): a window of
+    8 segments from an unaligned k, one search vs per-segment searches, N = 6."""
+    nonce, wb, wbits, ntz = [2, 2, 2, 2], 5, 3, 6
+    k0 = (1 << 24) + 4321
+    k1 = k0 + 8 * (1 << 24)
+    span = _all_hits(miner, nonce, ntz, wb, wbits, k0, k1)
+    per, k = [], k0
+    while k < k1:
+        ke = min(k1, ((k >> 24) + 1) << 24)
+        per += _all_hits(miner, nonce, ntz, wb, wbits, k, ke)
+        k = ke
+    assert span == per and len(span) >= 8 * 4
+
+
+def test_deep_hits_golden(miner, golden):
+    """N = 9 / 10 first hits (tests/golden/gen_golden.py --deep): BASELINE config 5's fresh
+    nonces seeded random.Random(416) at N = 9, the
+    config-1/2/5 nonces at N = 9 and [1,2,3,4] at N = 10 -- the full-digest path
+    (C word, then B, A) that N > 8 needs beyond the D-word test (worker.go:246-256)."""
+    deep = golden["deep_hits"]
+    assert {tuple(e["nonce"]) for e in deep if e["case"].startswith("config5-fresh")} == \
+        {(129, 3, 150, 161), (226, 19, 170, 24), (111, 251, 228, 114), (199, 4, 151, 255)}
+    for e in deep:
+        r = miner.mine(e["nonce"], e["ntz"])
+        assert r.status == FOUND, e
+        assert (r.global_idx, list(r.secret)) == (e["global_idx"], e["secret"]), (e, r)
+        assert _hexz(e["nonce"], r.secret) == e["md5"] and e["md5"].endswith("0" * e["ntz"])
+
+
+def test_n10_min_over_8_partitions(miner, golden):
+    """N = 10 on [1,2,3,4] (1.1e12 candidates expected; about 5 s per pass): the minimum of
+    the 8 workerBits = 3 partitions' first hits is the workerBits = 0 golden, and the
+    N = 9 first hit comes no later."""
+    e = next(x for x in golden["deep_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 10)
+    g10 = e["global_idx"]
+    k_stop = (g10 >> 8) + 1
+    hits = []
+    for wb in range(8):
+        r = miner.search([1, 2, 3, 4], 10, wb, 3, 0, k_stop)
+        if r.status == FOUND:
+            assert _tz([1, 2, 3, 4], r.secret) >= 10
+            hits.append((r.global_idx, wb))
+    assert min(hits) == (g10, (g10 & 255) >> 5)
+    e9 = next(x for x in golden["deep_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 9)
+    assert e9["global_idx"] <= g10
+    r9 = miner.search([1, 2, 3, 4], 9, 0, 0, 0, k_stop)
+    assert r9.status == FOUND and r9.global_idx == e9["global_idx"]

@@ -58,11 +58,14 @@ def test_plan_window_segments():
     for p in pl:
         assert (p.nblk, p.w0, p.sh) == (1, 1, 0)  # 4-byte nonce: V lands in word 1
         assert p.i_begin == p.k_begin * 256 and p.i_end == p.k_end * 256
-    # L >= 4 windows split at every multiple of 2^24 (constant high chunk bytes)
+    # L >= 4: one launch spans the 2^24-k segments (the kernel re-derives the constants
+    # of the words holding k >> 24); windows split only where the chunk length changes
     pl = distpow.plan_window(b"ab", 2, 2, (3 << 24) - 7, (5 << 24) + 3)
-    assert [(p.k_begin, p.k_end) for p in pl] == [((3 << 24) - 7, 3 << 24), (3 << 24, 4 << 24),
-                                                  (4 << 24, 5 << 24), (5 << 24, (5 << 24) + 3)]
+    assert [(p.k_begin, p.k_end, p.chunk_len) for p in pl] == [((3 << 24) - 7, (5 << 24) + 3, 4)]
     assert all(p.i_begin == p.k_begin * 64 for p in pl)
+    pl = distpow.plan_window(b"ab", 0, 0, (1 << 32) - 9, (1 << 32) + 2 * (1 << 24))
+    assert [(p.k_begin, p.k_end, p.chunk_len) for p in pl] == [((1 << 32) - 9, 1 << 32, 4),
+                                                               (1 << 32, (1 << 32) + (2 << 24), 5)]
     # beyond the k limit
     with pytest.raises(distpow.DpowError):
         distpow.plan_window(b"x", 0, 0, 0, (1 << 40) + 1)

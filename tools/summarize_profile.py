@@ -5,9 +5,9 @@
 
 Writes:
   <out>_kernel_stats.csv   rocprofv3 --stats table of the bench command (copied)
-  <out>_summary.json       per-kernel averages over the sweep launches (grid of the
-                           2^32-candidate launches), PMC-derived VALU instructions per
-                           candidate, effective clock, and HBM bytes per launch.
+  <out>_summary.json       per-kernel averages over the timed sweep launches, PMC-derived
+                           VALU instructions per candidate, effective clock, and the
+                           FETCH_SIZE / WRITE_SIZE bytes per launch (uncorrected).
 """
 import collections
 import csv
@@ -53,7 +53,7 @@ def main():
         "all_md5_avg_launch_ms": sum(dur) / len(dur),
         "sweep_launch_grid_threads": big,
         "sgpr_count": int(sweep[0]["SGPR_Count"]), "vgpr_count": int(sweep[0]["VGPR_Count"]),
-        "candidates_per_sweep_launch": 1 << 32,
+        "candidates_per_sweep_launch": int(bench["roofline"]["candidates_per_launch"]),
     }
     pmc = {}
     for name in ("pmc_sq", "pmc_fetch", "pmc_write"):
@@ -65,7 +65,7 @@ def main():
                         pmc.setdefault(k, []).append(v)
     if pmc:
         avg = {k: sum(v) / len(v) for k, v in pmc.items()}
-        n = 1 << 32
+        n = summary["candidates_per_sweep_launch"]
         if "SQ_INSTS_VALU" in avg:
             summary["valu_insts_per_candidate"] = avg["SQ_INSTS_VALU"] * 64 / n
             summary["salu_insts_per_candidate"] = avg["SQ_INSTS_SALU"] * 64 / n
@@ -81,16 +81,17 @@ def main():
             rate = avg["SQ_INSTS_VALU"] / 1024 / cyc
             summary["valu_insts_per_simd_cycle"] = rate
             summary["valu_busy_issue_model"] = rate * (236 * 4 + 258 * 2) / 494
-        # FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM section): on gfx950
-        # FETCH_SIZE reports half the bytes of coalesced reads (x2 before comparing with a byte
-        # count); WRITE_SIZE is exact for streaming stores and one-dword atomics.  This kernel's
-        # few accesses (kernarg scalar loads, one-lane 64-bit claim atomics) are of uncalibrated
-        # widths, so the figure is an order of magnitude, not an exact count.
+        # FETCH_SIZE / WRITE_SIZE are in KiB.  Reported uncorrected: MI355X_MICROARCH.md's x2
+        # FETCH_SIZE correction is calibrated on wide coalesced streaming reads, and this kernel
+        # has none -- its few accesses are kernarg scalar loads, one-lane 64-bit claim atomics
+        # (returning, 32-byte granules) and the completion records.  Algorithmic HBM bytes per
+        # candidate: 0.  The figure is the size of that control traffic, not a bandwidth load.
         if "FETCH_SIZE" in avg:
-            summary["fetch_bytes_per_launch"] = avg["FETCH_SIZE"] * 1024 * 2
-            summary["fetch_correction"] = "x2 (gfx950 FETCH_SIZE half-count, MI355X_MICROARCH.md)"
+            summary["fetch_bytes_per_launch"] = avg["FETCH_SIZE"] * 1024
+            summary["fetch_correction"] = "none (no streaming reads; raw FETCH_SIZE KiB x 1024)"
         if "WRITE_SIZE" in avg:
             summary["write_bytes_per_launch"] = avg["WRITE_SIZE"] * 1024
+            summary["traffic_kind"] = "claim atomics + kernarg loads + completion records (no algorithmic HBM bytes)"
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             summary["hbm_bytes_per_launch"] = summary["fetch_bytes_per_launch"] + summary["write_bytes_per_launch"]
     json.dump(summary, open(out + "_summary.json", "w"), indent=1)

@@ -50,6 +50,12 @@ namespace dpow {
 #ifndef DPOW_NUM_SGPR
 #define DPOW_NUM_SGPR 72
 #endif
+#ifndef DPOW_NUM_SGPR_LONG
+#define DPOW_NUM_SGPR_LONG 96  // long-nonce and two-block layouts (kNumSgpr below)
+#endif
+#ifndef DPOW_SGPR_LONG_W0
+#define DPOW_SGPR_LONG_W0 8
+#endif
 // A wave polls Ctrl::best / Ctrl::stop every DPOW_POLL_WB wave-blocks of a
 // chunk (0: once per chunk).  profiles/r01_ab_poll.log: 0 / 12 / 16 / 32 ->
 // 216.3 / 217.8 / 218.3 / 218.6 GH/s, time-to-secret N=7 1.57 / 1.47 / 1.49 / 1.56 ms.
@@ -619,9 +625,21 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
     return kNoHitG;
 }
 
+// SGPR budget per layout.  The grid is 6 four-wave workgroups per CU (6 waves per
+// SIMD, dpow_api.cpp), so a budget that still admits 7 waves costs no occupancy.
+// The short-nonce layouts keep the round-1 budget (72: no spill in the hash
+// loop; 8 waves admitted, so the next queued launch's workgroups start beside a
+// draining one).  Layouts with many launch-uniform K + M constants -- long nonces
+// and two final blocks -- get 96: at 72 the compiler spills them to VGPR lanes
+// and reloads each with a v_readlane in every wave-block (tools/isa_loop.py:
+// 4-41 per wave-block; 0 at 96).
+// (The attribute takes no template-dependent value: two kernel templates share
+// one body, and md5_variant.hip instantiates the one kLongSgpr selects.)
+template <int NBLK, int W0>
+constexpr bool kLongSgpr = NBLK == 2 || W0 >= DPOW_SGPR_LONG_W0;
+
 template <int NBLK, int W0, int SH, bool EQ>
-__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR)))
-md5_search_kernel(const Launch L) {
+DPOW_DEV void search_body(const Launch &L) {
     if (blockIdx.x == 0) {  // dispatched first: the watcher
         watcher(L);
         return;
@@ -804,6 +822,18 @@ md5_search_kernel(const Launch L) {
         const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim);
     }
+}
+
+template <int NBLK, int W0, int SH, bool EQ>
+__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR)))
+md5_search_kernel(const Launch L) {
+    search_body<NBLK, W0, SH, EQ>(L);
+}
+
+template <int NBLK, int W0, int SH, bool EQ>
+__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR_LONG)))
+md5_search_kernel_lsgpr(const Launch L) {
+    search_body<NBLK, W0, SH, EQ>(L);
 }
 
 }  // namespace dpow

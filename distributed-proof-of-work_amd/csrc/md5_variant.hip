@@ -18,7 +18,14 @@ namespace {
 using KernelFn = void (*)(Launch);
 // [EQ][w0 - kW0Lo]: EQ kernels (the D-equality test, use_d_equality) exist for
 // one final block only.
-#define DPOW_K(w, e) md5_search_kernel<DPOW_VNBLK, w, DPOW_VSH, e>
+// The kernel of a layout: the long-SGPR-budget template for long nonces and two
+// final blocks (md5_search_kernel.h kLongSgpr); only the chosen one is instantiated.
+template <int NBLK, int W0, int SH, bool EQ>
+constexpr KernelFn kernel_of() {
+    if constexpr (kLongSgpr<NBLK, W0>) return md5_search_kernel_lsgpr<NBLK, W0, SH, EQ>;
+    else return md5_search_kernel<NBLK, W0, SH, EQ>;
+}
+#define DPOW_K(w, e) kernel_of<DPOW_VNBLK, w, DPOW_VSH, e>()
 #if DPOW_VNBLK == 1
 constexpr int kW0Lo = 0;
 #define DPOW_ROW(e) \

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not n10" > gpurun_out/r02_gpu_tests_b.log 2>&1 && \
+timeout -k 10 300 python3 tools/data_sweep.py 34 > gpurun_out/r02_data_sweep.log 2>&1 && \
+timeout -k 10 400 python3 tools/layout_sweep.py 34 > gpurun_out/r02_layout_sweep_b.log 2>&1

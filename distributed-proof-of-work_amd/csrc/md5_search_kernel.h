@@ -121,9 +121,13 @@ struct KConst {
 #if DPOW_SPAN && DPOW_POLL_WB == 0
 #error "DPOW_SPAN needs the grouped chunk loop (DPOW_POLL_WB > 0)"
 #endif
+// For SH != 0 word W0 + 1 also holds the top bytes of V; its K + M is then
+// wave-uniform per wave-block anyway (VarWords::hi_s, which carries the
+// segment addition too), so only SH = 0's W0 + 1 and SH = 3's W0 + 2 are
+// VGPR-held segment words.
 template <int NBLK, int W0, int SH>
 DPOW_DEV_CONST bool seg_word(int m) {
-    return DPOW_SPAN && (m == W0 + 1 || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2));
+    return DPOW_SPAN && ((SH == 0 && m == W0 + 1) || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2));
 }
 
 template <int NBLK, int W0, int SH>
@@ -208,7 +212,10 @@ DPOW_DEV void kconst_seg(KConst &kc, const Launch &L, uint32_t d1, uint32_t d2) 
 struct VarWords {
     uint32_t lo_s[kNC];  // wave-uniform part of V << 8*SH (word W0)
     uint32_t lo_v;       // per-lane part of V << 8*SH (the same for every slot)
-    uint32_t hi[kNC];    // V >> (32 - 8*SH), added for steps reading word W0+1
+    uint32_t hi_s[kNC];  // SH != 0: the wave-uniform part of word W0+1's addition -- V >> (32 - 8 SH)
+                         //  (uniform: a lane's k offset never carries into those bits) plus the
+                         //  segment addition d1
+    uint32_t lane_k;     // SH = 3: the per-lane part of V >> 8 (the lane's k offset; 0 when R >= 64)
     const KConst *kc;    // launch-uniform K + M constants held in VGPRs (segment words: current segment)
     uint32_t seg_d[2];   // segment-word additions for the steps that read them from L.KT (full_check's
                          //  steps 62-63 of the last block only; the hash loop holds them all in kc)
@@ -223,14 +230,17 @@ struct StepWord {
     // word after W0 + 2 except the bit-length word -- are zero for every launch
     // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
     static constexpr bool zero_word = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
-    static constexpr bool per_lane = m == W0 || (SH != 0 && m == W0 + 1);
+    static constexpr bool per_lane = m == W0 || (SH == 3 && m == W0 + 1);  // K + M differs per lane
     static constexpr bool vgpr_k = VgprK<NBLK, W0, SH>::use(BLK, I);
     static constexpr bool seg = seg_word<NBLK, W0, SH>(m);
     static DPOW_DEV uint32_t km(const Launch &L, const VarWords &v, int j) {
         uint32_t k = zero_word ? kMd5K[I] : vgpr_k ? v.kc->v[64 * BLK + I] : L.KT[64 * BLK + I];
         if constexpr (seg && !vgpr_k) k += v.seg_d[m == W0 + 1 ? 0 : 1];
         if constexpr (m == W0) k = (k + v.lo_s[j]) + v.lo_v;
-        if constexpr (SH != 0 && m == W0 + 1) k += v.hi[j];
+        if constexpr (SH != 0 && m == W0 + 1) {
+            k += v.hi_s[j];                        // SALU: K + M stays uniform
+            if constexpr (SH == 3) k += v.lane_k;  // the one VALU add of the step
+        }
         return k;
     }
 };
@@ -490,12 +500,22 @@ DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords 
     }
 }
 
+// V = vs + loff (wave-uniform + per-lane) of slot j.  The lane offset holds the
+// thread-byte bits below R and the k bits below 64 / R; vs is zero in both
+// (i0 is a multiple of 64), so the sum never carries and V's bits above the
+// lane's k offset are wave-uniform: V >> 24 and V >> 16 are uniform, and
+// V >> 8 = (vs >> 8) + (loff >> 8).  d1 = the segment addition to word W0 + 1.
 template <int SH>
-DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff) {
+DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff, uint32_t d1) {
     v.lo_s[j] = vs << (8 * SH);
     v.lo_v = loff << (8 * SH);
-    if constexpr (SH != 0) v.hi[j] = (vs + loff) >> (32 - 8 * SH);
-    else v.hi[j] = 0;
+    if constexpr (SH != 0) {
+        v.hi_s[j] = (vs >> (32 - 8 * SH)) + d1;
+        v.lane_k = SH == 3 ? loff >> 8 : 0u;
+    } else {
+        v.hi_s[j] = 0u;
+        v.lane_k = 0u;
+    }
 }
 
 // Full digest test of one lane's candidate (rare path: only when the D-word
@@ -504,8 +524,8 @@ template <int NBLK, int W0, int SH>
 DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_t loff, uint64_t i0) {
     VarWords v;
     v.kc = &kc;
-    var_words<SH>(v, 0, vs, loff);
     seg_deltas<W0, SH>(L, (uint32_t)((i0 >> L.rbits) >> 24), v.seg_d[0], v.seg_d[1]);
+    var_words<SH>(v, 0, vs, loff, v.seg_d[0]);
     uint32_t out[4][kNC];
     md5_tail<NBLK, W0, SH, 1>(out, L, v);
     return trailing_zero_nibbles(out[0][0], out[1][0], out[2][0], out[3][0]) >= L.ntz;
@@ -583,10 +603,15 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
     VarWords v;
     v.kc = &kc;
     v.seg_d[0] = v.seg_d[1] = 0u;  // unused: the hash loop's segment-word steps all read kc
+    uint32_t d1 = 0u;               // SH != 0: the segment addition to word W0 + 1 (both slots share
+    if constexpr (SH != 0) {        //  the segment: wave-blocks never straddle one)
+        uint32_t d2;
+        seg_deltas<W0, SH>(L, (uint32_t)((i0 >> L.rbits) >> 24), d1, d2);
+    }
 #pragma unroll
     for (int j = 0; j < kNC; ++j) {
         vs[j] = wave_uniform_v(i0 + 64u * j, L.rbits, L.base_tb);
-        var_words<SH>(v, j, vs[j], loff);
+        var_words<SH>(v, j, vs[j], loff, d1);
     }
     uint32_t dig[4][kNC];
     md5_tail<NBLK, W0, SH, kNC, true, EQ>(dig, L, v);  // only D is tested here

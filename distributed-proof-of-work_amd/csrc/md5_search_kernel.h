@@ -165,11 +165,15 @@ struct VgprK {
     }
     // VGPRs the layout uses without VGPR constants (-Rpass-analysis=kernel-resource-usage):
     // one block 34-39 (SH = 0) / 43-49 (SH != 0), two blocks 41-43 / 49-53; each
-    // constant costs about one more.  The caps keep every kernel at <= 64; the
-    // segment-word constants count against them first.
+    // constant costs about one more.  The grid runs 6 waves per SIMD, so up to 80
+    // VGPRs cost no occupancy that is used; the caps keep every kernel within 72
+    // (7 waves: a queued launch's workgroups still start beside a draining one).
+    // The segment-word constants count against them first.  Round 1's caps for
+    // <= 64 VGPRs (14 one-block / 10 two-block for SH != 0) left the two-block
+    // layouts with 4-11 SGPR spill reloads per wave-block.
     static constexpr int kCap = DPOW_VGPR_K_MAX >= 0 ? DPOW_VGPR_K_MAX
-                                : NBLK == 1 ? (SH == 0 ? 24 : 14)
-                                            : (SH == 0 ? 20 : 10);
+                                : NBLK == 1 ? (SH == 0 ? 24 : SH == 3 ? 14 : 18)
+                                            : (SH == 3 ? 20 : 26);
     static constexpr bool use(int blk, int i) {
         return seg(blk, i) || (DPOW_VGPR_K && count() >= DPOW_VGPR_K_MIN && eligible(blk, i) &&
                                rank(blk, i) < kCap - count_seg());

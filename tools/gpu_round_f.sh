@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest tests/test_baseline_configs.py tests/test_gpu_node.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r02_gpu_tests_f.log 2>&1 && \
+timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --same-device --no-probe > gpurun_out/r02_bench_n2_rehearsal.json 2> gpurun_out/r02_bench_n2_rehearsal.err

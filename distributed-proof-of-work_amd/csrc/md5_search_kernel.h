@@ -130,12 +130,55 @@ DPOW_DEV_CONST bool seg_word(int m) {
     return DPOW_SPAN && ((SH == 0 && m == W0 + 1) || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2));
 }
 
+// First hand-ordered step of block 0: W0 + pipe_lead<NBLK, W0, SH>.  4 is the first
+// step whose four state words are all per-lane; before it the compiler schedules
+// the steps (some state words are wave-uniform there, and it exploits that).
+// Which start issues best depends on the layout; the table is the argmax of a
+// per-layout sweep of builds with one start for every layout
+// (DPOW_PIPE_LEAD = 1..6, tools/lead_sweep.py, profiles/r02_lead_sweep.json),
+// where a start beats 4 by >= 0.8 %.  The headline <1,1,0> keeps 4.
+// DPOW_PIPE_LEAD > 0 forces one start for every layout (A/B builds).
+#ifndef DPOW_PIPE_LEAD
+#define DPOW_PIPE_LEAD 0
+#endif
+constexpr int pipe_lead(int nblk, int w0, int sh) {
+    if (DPOW_PIPE_LEAD > 0) return DPOW_PIPE_LEAD;
+    if (nblk == 1) {
+        switch (w0 * 4 + sh) {
+            case 0 * 4 + 0: return 2;  // +1.3 %
+            case 2 * 4 + 0: return 3;  // +2.0 %
+            case 2 * 4 + 1: return 2;  // +0.8 %
+            case 2 * 4 + 2: return 2;  // +0.9 %
+            case 3 * 4 + 0: return 3;  // +2.2 %
+            case 3 * 4 + 3: return 1;  // +2.0 %
+            case 4 * 4 + 3: return 2;  // +1.0 %
+            case 8 * 4 + 3: return 3;  // +2.2 %
+            case 9 * 4 + 0: return 2;  // +3.7 %
+            case 9 * 4 + 3: return 3;  // +1.6 %
+            case 10 * 4 + 1: return 3; // +0.8 %
+            case 10 * 4 + 2: return 3; // +1.0 %
+            case 10 * 4 + 3: return 5; // +1.8 %
+            default: return 4;
+        }
+    }
+    switch (w0 * 4 + sh) {
+        case 12 * 4 + 3: return 1;  // +4.3 %
+        case 14 * 4 + 1: return 2;  // +5.0 %
+        case 14 * 4 + 2: return 2;  // +5.1 %
+        case 14 * 4 + 3: return 1;  // +4.3 %
+        case 15 * 4 + 0: return 2;  // +4.5 %
+        case 15 * 4 + 3: return 1;  // +5.7 %
+        default: return 4;
+    }
+}
+
 template <int NBLK, int W0, int SH>
 struct VgprK {
     // First step of block 0 in the hand-ordered pipeline (md5_tail's kI0 for
     // the hash loop's ONLY_D call with kNC candidates).
     static constexpr int kEnd0 = NBLK == 1 ? 62 : 64;
-    static constexpr int kI0 = W0 + 4 < kEnd0 ? W0 + 4 : kEnd0;
+    static constexpr int kLead = pipe_lead(NBLK, W0, SH);
+    static constexpr int kI0 = W0 + kLead < kEnd0 ? W0 + kLead : kEnd0;
     // Steps the hash loop runs (ONLY_D: the last block stops after step 61).
     static constexpr bool run(int blk, int i) { return !(blk == NBLK - 1 && i >= 62); }
     // Steps reading a segment word: always held in VGPRs (updated at segment changes).
@@ -376,7 +419,12 @@ template <int I> struct Roles {
     "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
 
 // One step pair of candidates p = J, q = J + 1 at step I (q finishes step I-1,
-// whose add3 is in tq, and starts step I).
+// whose add3 is in tq, and starts step I).  p's state word a is written in the
+// middle of the group (`+&v`, early-clobber): where the pipeline starts before
+// W0 + 4, p's and q's state words can still be the same wave-uniform value, and a
+// plain `+v` lets the register allocator hand q's input that same register, which
+// the group then overwrites before q reads it (a wrong hash in <1,0,0> at start
+// W0 + 2, caught by test_nonce_lengths_golden / tools/layout_check.py).
 template <int NBLK, int W0, int SH, int BLK, int I, int J>
 DPOW_DEV void body(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const VarWords &v) {
     using R = Roles<I>;  // q's step I-1 writes x[R::b][q] from x[R::c][q]
@@ -385,14 +433,14 @@ DPOW_DEV void body(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const V
     uint32_t fp, fq, rq, tp;
     if constexpr (W::per_lane || W::vgpr_k)
         asm volatile(DPOW_PIPE_BODY
-                     : [pa] "+v"(x[R::a][J]), [qb] "=&v"(x[R::b][J + 1]), [tq] "+v"(tq), [fp] "=&v"(fp),
+                     : [pa] "+&v"(x[R::a][J]), [qb] "=&v"(x[R::b][J + 1]), [tq] "+v"(tq), [fp] "=&v"(fp),
                        [fq] "=&v"(fq), [rq] "=&v"(rq), [tp] "=&v"(tp)
                      : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qc] "v"(x[R::c][J + 1]),
                        [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "v"(kp), [kq] "v"(kq),
                        [tt] "i"(tt<I>()), [sp] "i"(32 - md5_shift(I)), [sq] "i"(32 - md5_shift(I - 1)));
     else
         asm volatile(DPOW_PIPE_BODY
-                     : [pa] "+v"(x[R::a][J]), [qb] "=&v"(x[R::b][J + 1]), [tq] "+v"(tq), [fp] "=&v"(fp),
+                     : [pa] "+&v"(x[R::a][J]), [qb] "=&v"(x[R::b][J + 1]), [tq] "+v"(tq), [fp] "=&v"(fp),
                        [fq] "=&v"(fq), [rq] "=&v"(rq), [tp] "=&v"(tp)
                      : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qc] "v"(x[R::c][J + 1]),
                        [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "s"(kp), [kq] "s"(kq),
@@ -408,13 +456,13 @@ DPOW_DEV void prologue(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, con
     uint32_t fp, fq, tp;
     if constexpr (W::per_lane || W::vgpr_k)
         asm volatile(DPOW_PIPE_PRO
-                     : [pa] "+v"(x[R::a][J]), [tq] "=&v"(tq), [fp] "=&v"(fp), [fq] "=&v"(fq), [tp] "=&v"(tp)
+                     : [pa] "+&v"(x[R::a][J]), [tq] "=&v"(tq), [fp] "=&v"(fp), [fq] "=&v"(fq), [tp] "=&v"(tp)
                      : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qb] "v"(x[R::b][J + 1]),
                        [qc] "v"(x[R::c][J + 1]), [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "v"(kp),
                        [kq] "v"(kq), [tt] "i"(tt<I0>()), [sp] "i"(32 - md5_shift(I0)));
     else
         asm volatile(DPOW_PIPE_PRO
-                     : [pa] "+v"(x[R::a][J]), [tq] "=&v"(tq), [fp] "=&v"(fp), [fq] "=&v"(fq), [tp] "=&v"(tp)
+                     : [pa] "+&v"(x[R::a][J]), [tq] "=&v"(tq), [fp] "=&v"(fp), [fq] "=&v"(fq), [tp] "=&v"(tp)
                      : [pb] "v"(x[R::b][J]), [pc] "v"(x[R::c][J]), [pd] "v"(x[R::d][J]), [qb] "v"(x[R::b][J + 1]),
                        [qc] "v"(x[R::c][J + 1]), [qd] "v"(x[R::d][J + 1]), [qa] "v"(x[R::a][J + 1]), [kp] "s"(kp),
                        [kq] "s"(kq), [tt] "i"(tt<I0>()), [sp] "i"(32 - md5_shift(I0)));
@@ -475,12 +523,13 @@ DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords 
     for (int j = 0; j < NCAND; ++j) {
         x[0][j] = L.iv[0]; x[1][j] = L.iv[1]; x[2][j] = L.iv[2]; x[3][j] = L.iv[3];
     }
-    // The pipelined order needs all four state words per lane: from step W0 + 4
-    // of the first block on (earlier steps are wave-uniform or partly so, and
-    // the compiler folds them).
+    // The hand-ordered pipeline starts at step W0 + pipe_lead of the first block
+    // (all four state words are per-lane from W0 + 4 on; earlier steps are
+    // wave-uniform or partly so, and the compiler folds them).
     constexpr bool kPipe = DPOW_PIPE && NCAND == kNC && (kNC == 2 || kNC == 4);
     constexpr int kEnd0 = (ONLY_D && NBLK == 1) ? 62 : 64;
-    constexpr int kI0 = kPipe ? (W0 + 4 < kEnd0 ? W0 + 4 : kEnd0) : kEnd0;
+    constexpr int kLead = pipe_lead(NBLK, W0, SH);
+    constexpr int kI0 = kPipe ? (W0 + kLead < kEnd0 ? W0 + kLead : kEnd0) : kEnd0;
     md5_steps<NBLK, W0, SH, 0, 0, kI0, NCAND>(x, L, v);
     if constexpr (kPipe) pipe::steps<NBLK, W0, SH, 0, kI0, kEnd0>(x, L, v);
 #pragma unroll

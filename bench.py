@@ -39,7 +39,7 @@ CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 STRONG_TOTAL_PER_STEP = 1 << 38    # --strong: fixed total work per step
 K0 = 1 << 24                      # start of the L = 4 segment
 PROFILE_TAG = "r02"                # profiles/<tag>_summary.json of the current kernel
-TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x4 up to 2^22 k
+TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x4 up to 2^29 candidates per rank
 TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first_ms: the first, cold)
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
 # INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,

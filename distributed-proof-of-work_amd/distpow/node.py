@@ -49,22 +49,27 @@ def owner_rank(global_idx: int, world: int) -> int:
 def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
               batch_k: int = 1 << 8, k_start: int = 0, k_limit: int = DPOW_K_LIMIT, group=None,
               device=None, cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
-              batch_k_max: int = 1 << 22) -> NodeResult:
+              batch_k_max: Optional[int] = None, batch_candidates_max: int = 1 << 29) -> NodeResult:
     """Search until the first hit of the whole node (deterministic) or a cancel vote.
 
     search_fn(nonce, ntz, worker_byte, worker_bits, k_begin, k_end, bound) -> SearchResult
     is this rank's one-window search (Miner.search for the GPU product).
 
-    Batches start at batch_k chunks and grow by `growth` up to batch_k_max.  Every rank
-    must finish a batch before the all-reduce, so a batch bounds the overshoot past the
-    hit: small first batches keep small N at a few short batches, and the cap keeps
-    the overshoot at large N to one batch (2^22 k x 32 thread bytes at 8 GPUs = 0.65 ms
-    of hashing per rank), ~10x the per-batch all-reduce and host round trip.
+    Batches start at batch_k chunks and grow by `growth` up to batch_k_max (default:
+    batch_candidates_max = 2^29 candidates per rank, 2.5 ms of hashing; 2^24 k at 8
+    GPUs).  Every rank must finish a batch before the all-reduce, so a batch bounds the
+    overshoot past the hit: small first batches keep small N at a few short batches.
+    The cap trades the per-batch cost c (the window's launch and drain, the all-reduce
+    and the host round trip, ~0.1 ms) against the overshoot (about half the last batch):
+    for T ms of hashing per rank the sum c T / B + B / 2 is smallest near B = sqrt(2 c T),
+    2.3 ms for N = 9 at 8 GPUs (~26 ms per rank).  (Round 1 capped at 2^22 k, 0.6 ms.)
     """
     import torch
     import torch.distributed as dist
 
     wb, wbits = partition_of_rank(rank, world)
+    if batch_k_max is None:
+        batch_k_max = max(1, batch_candidates_max >> (8 - wbits % 9))
     dist_on = world > 1 and dist.is_available() and dist.is_initialized()
     if device is None:
         backend = dist.get_backend(group) if dist_on else "gloo"

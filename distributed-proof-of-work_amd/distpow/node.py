@@ -87,12 +87,13 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
         if r.status == FOUND:
             secret = r.secret
         running = 0 if (r.status == CANCELLED or cancelled()) else 1
-        buf[0] = mine
-        buf[1] = running
+        # one host->device copy in and one device->host copy out per batch (each is a
+        # synchronous round trip of tens of microseconds with RCCL's device tensors)
+        buf.copy_(torch.tensor([mine, running], dtype=torch.int64))
         if dist_on:
             dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
         batches += 1
-        best, all_running = int(buf[0].item()), int(buf[1].item())
+        best, all_running = (int(x) for x in buf.tolist())
         if best != DPOW_NO_HIT:
             own = owner_rank(best, world)
             if best != mine:

@@ -27,10 +27,8 @@
 #include "md5_host.h"
 #include "md5_variants.h"
 #include "plan.h"
+#include "../../include/dpow_diag.h"
 
-#ifndef DPOW_MAX_CHUNK
-#define DPOW_MAX_CHUNK 32
-#endif
 
 using namespace dpow;
 
@@ -69,13 +67,6 @@ int hip_fail(hipError_t e, const char *what) {
 #define DPOW_BLOCKS_PER_CU 6
 #endif
 constexpr uint64_t kBlocksPerCu = DPOW_BLOCKS_PER_CU;
-constexpr uint64_t kClaimsPerWave = 16;
-constexpr uint64_t kMinChunk = 4;
-constexpr uint64_t kMaxChunk = DPOW_MAX_CHUNK;
-#ifndef DPOW_TAIL_CLAIMS
-#define DPOW_TAIL_CLAIMS 2  // small claims per wave at the end of a launch (0: none; A/B switch)
-#endif
-constexpr uint64_t kTailClaimsPerWave = DPOW_TAIL_CLAIMS;
 // Claim-counter slots (kClaimSlot counters each) used round-robin by the launches
 // of a search: zeroed at search start, re-zeroed by each launch's last workgroup.
 constexpr size_t kClaimRing = 64;
@@ -331,6 +322,39 @@ int dpow_plan_candidate(const uint8_t *nonce, size_t nonce_len, uint32_t worker_
     return 0;
 }
 
+int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte, uint32_t worker_bits,
+                              uint64_t k_begin, uint64_t k_end, uint64_t max_blocks, dpow_diag_launch *out,
+                              size_t max_launches) {
+    WindowPlanner planner;
+    const int rc = planner.init(nonce, nonce_len, 0, worker_byte, worker_bits, k_begin, k_end);
+    if (rc < 0) return set_error(rc, "dpow_diag_launch_geometry: bad arguments");
+    PlannedLaunch pl;
+    size_t n = 0;
+    while (planner.next(pl)) {
+        uint64_t wblocks = 0;
+        const int r = size_launch(pl, max_blocks, &wblocks);
+        if (r < 0) return set_error(r, "dpow_diag_launch_geometry: launch grid leaves a claim counter without waves");
+        if (out && n < max_launches) {
+            dpow_diag_launch &d = out[n];
+            d.k_begin = pl.info.k_begin;
+            d.k_end = pl.info.k_end;
+            d.i_begin = pl.L.i_begin;
+            d.i_end = pl.L.i_end;
+            d.wb_begin = pl.L.wb_begin;
+            d.n_wblocks = pl.L.n_wblocks;
+            d.n_big = pl.L.n_big;
+            d.n_chunks = pl.L.n_chunks;
+            d.worker_blocks = wblocks;
+            d.chunk = pl.L.chunk;
+            d.chunk_tail = pl.L.chunk_tail;
+            d.rbits = pl.L.rbits;
+            d.wave_block = kWaveBlock;
+        }
+        ++n;
+    }
+    return (int)n;
+}
+
 int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint64_t k, uint32_t iv_d,
                          uint32_t state_d) {
     std::vector<PlannedLaunch> plan;
@@ -375,7 +399,6 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot), bound, c->stream);
     if (e != hipSuccess) return hip_fail(e, "search_reset");
 
-    constexpr uint32_t wpb = kBlockThreads / 64;
     const uint64_t seq0 = c->seq;
     uint32_t done_target = 0;
     size_t launched = 0, consumed = 0;
@@ -414,44 +437,13 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         LaunchSlot &slot = c->slots[seq % kRing];
         if (harvest(c, slot) < 0) return DPOW_EHIP;  // the slot's previous launch
         Launch &L = pl.L;
-        uint64_t worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
         // This search's share of the device's resident workgroups (1 / searches in flight on it).
         const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
         const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * kBlocksPerCu / share, kClaimCounters);
-        if (worker_blocks > max_blocks) worker_blocks = max_blocks;
-        uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
-        if (chunk < kMinChunk) chunk = kMinChunk;
-        if (chunk > kMaxChunk) chunk = kMaxChunk;
-        if (DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) {
-            // The launch spans 2^24-k segments: a power-of-two chunk and wave-blocks
-            // counted from a multiple of chunk wave-blocks put every segment boundary
-            // (a multiple of 2^24 * R indices) on a claim boundary, big or tail, so
-            // no chunk straddles one (the kernel switches constants per chunk group).
-            while (chunk & (chunk - 1)) chunk &= chunk - 1;
-            L.wb_begin = L.i_begin & ~(chunk * (uint64_t)kWaveBlock - 1);
-            L.n_wblocks = (L.i_end - L.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
-        }
-        // Guided tail: the last ~kTailClaimsPerWave claims per wave are
-        // kMinChunk wave-blocks, so the waves of a launch run dry together.
-        const uint64_t chunk_tail = kMinChunk < chunk ? kMinChunk : chunk;
-        const uint64_t tail_wb = worker_blocks * wpb * kTailClaimsPerWave * chunk_tail;
-        const uint64_t n_big = L.n_wblocks > tail_wb ? (L.n_wblocks - tail_wb) / chunk : 0;
-        const uint64_t rest = L.n_wblocks - n_big * chunk;
-        const uint64_t n_chunks = n_big + (rest + chunk_tail - 1) / chunk_tail;
-        // No more waves than chunks, but a worker block for every counter that
-        // holds a chunk (block b serves counter (b - 1) % kClaimCounters).
-        uint64_t need_blocks = (n_chunks + wpb - 1) / wpb;
-        if (need_blocks < n_chunks && need_blocks < kClaimCounters)
-            need_blocks = n_chunks < kClaimCounters ? n_chunks : kClaimCounters;
-        if (worker_blocks > need_blocks) worker_blocks = need_blocks;
-        if (worker_blocks < kClaimCounters && worker_blocks < n_chunks)
-            return set_error(DPOW_EINVAL, "dpow_search: launch grid leaves a claim counter without waves");
+        uint64_t worker_blocks = 0;
+        rc = size_launch(pl, max_blocks, &worker_blocks);
+        if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
-        L.chunk = (uint32_t)chunk;
-        L.chunk_tail = (uint32_t)chunk_tail;
-        L.n_big = n_big;
-        L.n_chunks = n_chunks;
-        L.n_head = 2 * worker_blocks * wpb;
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;

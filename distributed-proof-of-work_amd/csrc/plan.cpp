@@ -140,4 +140,48 @@ void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words
     }
 }
 
+int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks_out) {
+    Launch &L = pl.L;
+    constexpr uint64_t wpb = kBlockThreads / 64;
+    // Chunk: >= kClaimsPerWave claims per wave of the largest grid the launch gets.
+    uint64_t worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
+    if (worker_blocks > max_blocks) worker_blocks = max_blocks;
+    uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
+    if (chunk < kMinChunk) chunk = kMinChunk;
+    if (chunk > kMaxChunk) chunk = kMaxChunk;
+    if (DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) {
+        // The launch spans 2^24-k segments: a power-of-two chunk and wave-blocks
+        // counted from a multiple of chunk wave-blocks put every segment boundary
+        // (a multiple of 2^24 * R indices) on a claim boundary, big or tail, so no
+        // claim straddles one (the kernel switches constants per chunk group).
+        while (chunk & (chunk - 1)) chunk &= chunk - 1;
+        L.wb_begin = L.i_begin & ~(chunk * (uint64_t)kWaveBlock - 1);
+        L.n_wblocks = (L.i_end - L.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
+        // The realignment adds up to chunk - 1 wave-blocks: size the grid on the new count.
+        worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
+        if (worker_blocks > max_blocks) worker_blocks = max_blocks;
+    }
+    // Guided tail: the last ~kTailClaimsPerWave claims per wave are kMinChunk
+    // wave-blocks, so the waves of a launch run dry together.
+    const uint64_t chunk_tail = kMinChunk < chunk ? kMinChunk : chunk;
+    const uint64_t tail_wb = worker_blocks * wpb * kTailClaimsPerWave * chunk_tail;
+    const uint64_t n_big = L.n_wblocks > tail_wb ? (L.n_wblocks - tail_wb) / chunk : 0;
+    const uint64_t rest = L.n_wblocks - n_big * chunk;
+    const uint64_t n_chunks = n_big + (rest + chunk_tail - 1) / chunk_tail;
+    // No more waves than claims, but a worker block for every counter that holds
+    // a claim (block b serves counter (b - 1) % kClaimCounters).
+    uint64_t need_blocks = (n_chunks + wpb - 1) / wpb;
+    if (need_blocks < n_chunks && need_blocks < kClaimCounters)
+        need_blocks = n_chunks < kClaimCounters ? n_chunks : kClaimCounters;
+    if (worker_blocks > need_blocks) worker_blocks = need_blocks;
+    if (worker_blocks < kClaimCounters && worker_blocks < n_chunks) return DPOW_EINVAL;
+    L.chunk = (uint32_t)chunk;
+    L.chunk_tail = (uint32_t)chunk_tail;
+    L.n_big = n_big;
+    L.n_chunks = n_chunks;
+    L.n_head = 2 * worker_blocks * wpb;
+    *worker_blocks_out = worker_blocks;
+    return 0;
+}
+
 }  // namespace dpow

@@ -42,4 +42,25 @@ int plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t w
 
 void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words[32]);
 
+// Claim geometry of a launch (dpow_search; CPU-testable through
+// dpow_diag_launch_geometry): chunk sizes, the guided tail, the claim count and
+// the worker workgroups (at most max_blocks, at least one per claim counter that
+// holds a claim); a launch spanning 2^24-k segments gets its wave-blocks counted
+// from a multiple of a power-of-two chunk, so no claim straddles a segment.
+// Fills pl.L.{wb_begin, n_wblocks, chunk, chunk_tail, n_big, n_chunks, n_head};
+// returns 0, or DPOW_EINVAL if a claim counter would be left without waves.
+constexpr uint64_t kClaimsPerWave = 16;   // big claims per wave (chunk sizing)
+constexpr uint64_t kMinChunk = 4;         // wave-blocks per claim: at least ...
+#ifndef DPOW_MAX_CHUNK
+#define DPOW_MAX_CHUNK 32
+#endif
+constexpr uint64_t kMaxChunk = DPOW_MAX_CHUNK;  // ... and at most
+#ifndef DPOW_TAIL_CLAIMS
+#define DPOW_TAIL_CLAIMS 2  // small claims per wave at the end of a launch (0: none; A/B switch)
+#endif
+constexpr uint64_t kTailClaimsPerWave = DPOW_TAIL_CLAIMS;
+static_assert((kMinChunk & (kMinChunk - 1)) == 0 && (kMaxChunk & (kMaxChunk - 1)) == 0,
+              "chunk bounds are powers of two (segment alignment)");
+int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks);
+
 }  // namespace dpow

@@ -50,6 +50,26 @@ int dpow_diag_launch_latency(int device, int mode, int reps, double *median_us);
 int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint64_t k,
                          uint32_t iv_d, uint32_t state_d);
 
+/* Claim geometry dpow_search gives each launch of a window (host logic, no GPU):
+ * the planner's launches sized for a grid of at most max_blocks worker workgroups
+ * (dpow_search passes CUs x 6 / searches in flight on the device).  One entry per
+ * launch; returns the number of launches (only the first max_launches are written),
+ * or < 0 when a launch would leave a claim counter without waves. */
+typedef struct dpow_diag_launch {
+    uint64_t k_begin, k_end;      /* chunk range */
+    uint64_t i_begin, i_end;      /* local index range */
+    uint64_t wb_begin;            /* first wave-block's local index */
+    uint64_t n_wblocks;           /* wave-blocks from wb_begin covering i_end */
+    uint64_t n_big, n_chunks;     /* claims of `chunk` wave-blocks, all claims */
+    uint64_t worker_blocks;       /* worker workgroups launched (plus the watcher) */
+    uint32_t chunk, chunk_tail;   /* wave-blocks per big / tail claim */
+    uint32_t rbits;               /* R = 2^rbits thread bytes per k */
+    uint32_t wave_block;          /* local indices per wave-block */
+} dpow_diag_launch;
+int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte,
+                              uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,
+                              uint64_t max_blocks, dpow_diag_launch *out, size_t max_launches);
+
 #ifdef __cplusplus
 }
 #endif

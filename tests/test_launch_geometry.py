@@ -1,0 +1,103 @@
+"""Claim geometry of dpow_search's launches (host logic; no GPU): plan.cpp size_launch via
+dpow_diag_launch_geometry.  Invariants the kernel relies on (md5_search_kernel.h):
+
+* the wave-blocks from wb_begin (a multiple of the wave-block size, <= i_begin) cover
+  i_end, and the claims -- n_big of `chunk` wave-blocks, then tail claims of
+  `chunk_tail` -- cover exactly those wave-blocks;
+* every claim counter that holds a claim has a worker workgroup (block b serves
+  counter (b - 1) % 8), and the grid never exceeds max_blocks;
+* in a launch that spans 2^24-k segments no claim straddles a segment boundary (the
+  kernel re-derives the segment words' constants per claim group).
+
+Round 2's parity soak found a launch of a few wave-blocks across a 2^24-k boundary
+whose realigned wave-block count left a counter without waves; these cases pin it.
+"""
+import ctypes
+import random
+
+import pytest
+
+import distpow
+
+CLAIM_COUNTERS = 8
+WPB = 4  # waves per workgroup
+
+
+class DiagLaunch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("k_begin", "k_end", "i_begin", "i_end", "wb_begin", "n_wblocks",
+                                                "n_big", "n_chunks", "worker_blocks")] + \
+               [(n, ctypes.c_uint32) for n in ("chunk", "chunk_tail", "rbits", "wave_block")]
+
+
+def geometry(nonce, wb, wbits, k0, k1, max_blocks):
+    L = distpow.lib()
+    fn = L.dpow_diag_launch_geometry
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                   ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(DiagLaunch), ctypes.c_size_t]
+    n = bytes(nonce)
+    arr = (DiagLaunch * 16)()
+    cnt = fn(n, len(n), wb, wbits, k0, k1, max_blocks, arr, 16)
+    assert cnt >= 0, distpow._lib.last_error()
+    return list(arr[:cnt])
+
+
+def check(d, max_blocks):
+    W = d.wave_block
+    assert d.wb_begin % W == 0 and d.wb_begin <= d.i_begin < d.i_end
+    assert d.wb_begin + d.n_wblocks * W >= d.i_end > d.wb_begin + (d.n_wblocks - 1) * W
+    tails = d.n_chunks - d.n_big
+    covered = d.n_big * d.chunk + tails * d.chunk_tail
+    assert covered >= d.n_wblocks > covered - d.chunk_tail  # the last (tail) claim is the only partial one
+    holders = min(d.n_chunks, CLAIM_COUNTERS)
+    assert holders <= d.worker_blocks <= max(max_blocks, CLAIM_COUNTERS)
+    # no more workgroups than the claims need (one wave per claim, rounded up to a workgroup)
+    assert d.worker_blocks <= max(-(-d.n_chunks // WPB), holders)
+    seg_i = 1 << (24 + d.rbits)  # local indices per 2^24-k segment
+    if d.k_begin >> 24 != (d.k_end - 1) >> 24:
+        assert d.chunk & (d.chunk - 1) == 0 and d.chunk % d.chunk_tail == 0
+        assert d.wb_begin % (d.chunk * W) == 0  # claim starts fall on multiples of the claim size
+        starts = [(c * d.chunk, d.chunk) for c in range(min(d.n_big, 4000))]
+        starts += [(d.n_big * d.chunk + t * d.chunk_tail, d.chunk_tail) for t in range(min(tails, 4000))]
+        for s, sz in starts:
+            lo = d.wb_begin + s * W
+            hi = d.wb_begin + (s + sz) * W - 1
+            assert lo // seg_i == hi // seg_i, (d.k_begin, d.k_end, s, sz)
+
+
+@pytest.mark.parametrize("max_blocks", [8, 192, 1536])
+def test_boundary_straddling_windows(max_blocks):
+    rnd = random.Random(max_blocks)
+    for _ in range(400):
+        wbits = rnd.choice([0, 1, 2, 3, 5, 8, 9, 10])
+        wb = rnd.randrange(1 << (wbits % 9)) if wbits % 9 else 0
+        m = rnd.randrange(1, 300)
+        if rnd.random() < 0.5:
+            m += 256  # k >= 2^32 too (L = 5)
+        edge = m << 24
+        k0 = max(1 << 24, edge - rnd.randrange(1, 3000))
+        k1 = min(1 << 40, edge + rnd.randrange(1, 3000))
+        nonce = [rnd.randrange(256) for _ in range(rnd.choice([0, 3, 4, 7, 55, 60, 64]))]
+        for d in geometry(nonce, wb, wbits, k0, k1, max_blocks):
+            check(d, max_blocks)
+
+
+def test_large_and_small_windows():
+    rnd = random.Random(3)
+    for _ in range(300):
+        wbits = rnd.choice([0, 3, 8])
+        wb = rnd.randrange(1 << wbits) if wbits else 0
+        k0 = rnd.choice([0, 1, 255, 70000, (1 << 24) - 1, 1 << 24, rnd.randrange(1 << 32), (1 << 32) + 5])
+        k1 = min(1 << 40, k0 + rnd.choice([1, 2, 7, 64, 5000, 1 << 20, 1 << 26, 1 << 31]))
+        for max_blocks in (8, 1536):
+            for d in geometry([1, 2, 3, 4], wb, wbits, k0, k1, max_blocks):
+                check(d, max_blocks)
+
+
+def test_bench_step_is_one_launch():
+    """The bench step (2^28 k from 2^24 at workerBits 0) and an 8-GPU rank's step (2^31 k at
+    workerBits 3) are one launch each: launches span the 2^24-k segments."""
+    for wb, wbits, nk in ((0, 0, 1 << 28), (5, 3, 1 << 31)):
+        ds = geometry([1, 2, 3, 4], wb, wbits, 1 << 24, (1 << 24) + nk, 1536)
+        assert len(ds) == 1 and ds[0].chunk == 32 and ds[0].worker_blocks == 1536
+        check(ds[0], 1536)

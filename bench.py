@@ -31,7 +31,7 @@ import torch  # noqa: E402  (before libdpow: one shared HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import distpow  # noqa: E402
-from distpow.node import NodeResult, node_mine, partition_of_rank  # noqa: E402
+from distpow.node import NodeResult, node_mine, node_mine_async, partition_of_rank  # noqa: E402
 
 NONCE = [1, 2, 3, 4]
 SWEEP_NTZ = 32
@@ -41,6 +41,10 @@ K0 = 1 << 24                      # start of the L = 4 segment
 PROFILE_TAG = "r02"                # profiles/<tag>_summary.json of the current kernel
 TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x4 up to 2^29 candidates per rank
 TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first_ms: the first, cold)
+# N > 1 time-to-secret: node_mine (batch-synchronous, RCCL all-reduce at batch boundaries,
+# the GPUs idle during it) unless DPOW_NODE_ASYNC=1 selects node_mine_async (ticked all-reduce
+# beside the running kernels, bound injection).
+NODE_SYNC = os.environ.get("DPOW_NODE_ASYNC") != "1"
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
 # INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,
 # the MI355X_MICROARCH.md FP32 vector peak (157.3 TFLOP/s) / 2 FLOP per FMA lane-op.
@@ -152,9 +156,13 @@ def main():
             if world == 1:  # one rank: the miner's own pipelined windows, no batch boundaries
                 r = miner.mine(nonce, n)
                 res = NodeResult(r.status, r.global_idx, r.secret, 0, 0)
-            else:
+            elif NODE_SYNC:  # round 1's batch-synchronous node search
                 res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
                                 batch_k=TTS_BATCH_K, device=dev)
+            else:  # no batch boundaries: ticked all-reduce + the node's best injected into each rank's search
+                res = node_mine_async(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
+                                      bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
+                                      batch_k=TTS_BATCH_K, device=dev)
             barrier()
             runs.append((time.perf_counter() - t1) * 1e3)
             assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
@@ -243,6 +251,9 @@ def main():
             "stream_event_ms": round(stream_ms, 3),
             "valu_probe": probe,
             "time_to_secret": tts,
+            "time_to_secret_node_search": ("one rank: Miner.mine" if world == 1 else
+                                           "node_mine (batch-synchronous)" if NODE_SYNC else
+                                           "node_mine_async (ticked all-reduce, bound injection)"),
             **extra,
             "cpu_baseline": cpu,
             "geometry": {"cus": cus, "threads_per_block": tpb},

@@ -45,6 +45,10 @@ int hip_fail(hipError_t e, const char *what) {
     return set_error(DPOW_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Internal status of consume(): the window holds nothing below a bound injected
+// by dpow_search_bound (reported as DPOW_EXHAUSTED).
+constexpr int DPOW_BOUNDED = 3;
+
 #define DPOW_HIP(call)                                    \
     do {                                                  \
         hipError_t e_ = (call);                           \
@@ -120,6 +124,14 @@ struct dpow_ctx {
     uint64_t seq = 0;  // launches ever queued on this context (record/slot index = seq % kRing)
     LaunchSlot slots[kRing];
     dpow_stats stats{};
+    // External bound (dpow_search_bound): lowered from another thread while a
+    // search runs, applied to Ctrl::best by a one-thread atomicMin kernel on
+    // bound_stream, ordered after the search's reset kernel (reset_ev).
+    std::mutex bound_mu;
+    bool searching = false;                      // under bound_mu
+    std::atomic<uint64_t> ext_bound{DPOW_NO_HIT};  // the lowest bound injected into the running search
+    hipStream_t bound_stream = nullptr;
+    hipEvent_t reset_ev = nullptr;
 };
 
 namespace {
@@ -209,6 +221,8 @@ int dpow_open(int device, dpow_ctx **out) {
     }
     c->cus = (uint32_t)prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->bound_stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->reset_ev, hipEventDisableTiming)) != hipSuccess ||
         (e = hipMalloc(&c->d_ctrl, sizeof(Ctrl))) != hipSuccess ||
         (e = hipMalloc(&c->d_claims, kClaimRing * kClaimSlot * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_snap, kRing * sizeof(Snap), hipHostMallocCoherent | hipHostMallocMapped)) !=
@@ -244,6 +258,11 @@ void dpow_close(dpow_ctx *c) {
     if (c->h_snap) (void)hipHostFree(c->h_snap);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->bound_stream) {
+        (void)hipStreamSynchronize(c->bound_stream);
+        (void)hipStreamDestroy(c->bound_stream);
+    }
+    if (c->reset_ev) (void)hipEventDestroy(c->reset_ev);
     delete c;
 }
 
@@ -270,6 +289,20 @@ void dpow_reset_stats(dpow_ctx *c) {
     if (!c) return;
     (void)harvest_all(c);  // launches queued before the reset stay out of the new counts
     c->stats = dpow_stats{};
+}
+
+int dpow_search_bound(dpow_ctx *c, uint64_t global_idx) {
+    if (!c) return set_error(DPOW_EINVAL, "dpow_search_bound: ctx is NULL");
+    std::lock_guard<std::mutex> g(c->bound_mu);
+    if (!c->searching) return 0;  // no search in flight: the caller passes its bound to the next one
+    uint64_t cur = c->ext_bound.load(std::memory_order_relaxed);
+    if (global_idx >= cur) return 0;
+    c->ext_bound.store(global_idx, std::memory_order_release);
+    DPOW_HIP(hipSetDevice(c->device));
+    DPOW_HIP(hipStreamWaitEvent(c->bound_stream, c->reset_ev, 0));  // after this search's reset
+    const hipError_t e = search_bound(c->d_ctrl, global_idx, c->bound_stream);
+    if (e != hipSuccess) return hip_fail(e, "search_bound");
+    return 0;
 }
 
 int dpow_secret_from_index(uint64_t g, uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len) {
@@ -398,6 +431,24 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     const uint64_t bound = *best_global_idx;
     hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot), bound, c->stream);
     if (e != hipSuccess) return hip_fail(e, "search_reset");
+    DPOW_HIP(hipEventRecord(c->reset_ev, c->stream));
+    // Open the window for dpow_search_bound; closed (and its atomicMin kernels
+    // drained, so none lands on the next search's reset) on every return path.
+    struct BoundWindow {
+        dpow_ctx *c;
+        explicit BoundWindow(dpow_ctx *cc) : c(cc) {
+            std::lock_guard<std::mutex> g(c->bound_mu);
+            c->ext_bound.store(DPOW_NO_HIT, std::memory_order_relaxed);
+            c->searching = true;
+        }
+        ~BoundWindow() {
+            {
+                std::lock_guard<std::mutex> g(c->bound_mu);
+                c->searching = false;
+            }
+            (void)hipStreamSynchronize(c->bound_stream);
+        }
+    } bound_window(c);
 
     const uint64_t seq0 = c->seq;
     uint32_t done_target = 0;
@@ -416,6 +467,10 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         consumed = lj + 1;
         const Snap &sn = c->h_snap[seq % kRing];
         if (sn.best < bound) {
+            // Ctrl::best = min(this search's hits, bounds injected by dpow_search_bound).
+            // At or above the lowest injected bound it is not a hit of ours: nothing
+            // below that bound remains in the window, so the search is over.
+            if (sn.best >= c->ext_bound.load(std::memory_order_acquire)) return DPOW_BOUNDED;
             best = sn.best;
             return DPOW_FOUND;
         }
@@ -467,6 +522,7 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         if (r < 0) return r;
         status = r;
     }
+    if (status == DPOW_BOUNDED) status = DPOW_EXHAUSTED;  // no hit below the (injected) bound
     if (status == DPOW_CANCELLED && consumed < launched) {
         // Up to kDepth launches are still queued.  Mark them stale so their
         // watchers stop them even when the caller clears the cancel flag for

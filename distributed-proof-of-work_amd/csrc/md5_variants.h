@@ -31,6 +31,9 @@ inline bool variant_exists(int nblk, int w0, int sh) {
 hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream);
 hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu);
 
+// Lower a running search's Ctrl::best to an external bound (search_ctrl.hip).
+hipError_t search_bound(Ctrl *ctrl, unsigned long long g, hipStream_t stream);
+
 // Per-search reset of the control block and claim counters (search_ctrl.hip).
 hipError_t search_reset(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
                         hipStream_t stream);

@@ -21,7 +21,17 @@ __global__ void __launch_bounds__(kBlockThreads) search_reset_kernel(Ctrl *ctrl,
     }
     for (uint32_t i = threadIdx.x; i < n_claims; i += kBlockThreads) claims[i] = 0ull;
 }
+// Lower Ctrl::best to an external bound (dpow_search_bound) while a search runs:
+// its waves stop claiming work at or above it at their next group.
+__global__ void search_bound_kernel(Ctrl *ctrl, unsigned long long g) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_min(&ctrl->best, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 }  // namespace
+
+hipError_t search_bound(Ctrl *ctrl, unsigned long long g, hipStream_t stream) {
+    hipLaunchKernelGGL(search_bound_kernel, dim3(1), dim3(64), 0, stream, ctrl, g);
+    return hipGetLastError();
+}
 
 hipError_t search_reset(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
                         hipStream_t stream) {

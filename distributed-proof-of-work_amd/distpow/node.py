@@ -15,12 +15,14 @@ a deterministic reduction; the owner of the winning index is rank
 (threadByte >> (8 - b)), the worker that would have reported WorkerResult.
 """
 import math
+import threading
+import time
 from dataclasses import dataclass
 from typing import Callable, Optional, Sequence
 
 from ._lib import CANCELLED, DPOW_K_LIMIT, DPOW_NO_HIT, EXHAUSTED, FOUND
 
-__all__ = ["NodeResult", "node_mine", "partition_of_rank", "owner_rank"]
+__all__ = ["NodeResult", "node_mine", "node_mine_async", "partition_of_rank", "owner_rank"]
 
 
 @dataclass
@@ -104,3 +106,136 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
             return NodeResult(CANCELLED, batches=batches)
         k = ke
     return NodeResult(EXHAUSTED, batches=batches)
+
+
+def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
+                    bound_fn: Callable[[int], None] = lambda g: None, cancel_fn: Callable[[], None] = lambda: None,
+                    clear_fn: Callable[[], None] = lambda: None, batch_k: int = 1 << 8, k_start: int = 0,
+                    k_limit: int = DPOW_K_LIMIT, group=None, device=None,
+                    cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
+                    batch_candidates_max: int = 1 << 31, tick_s: float = 1e-4,
+                    sync_candidates: int = 1 << 27) -> NodeResult:
+    """node_mine without batch boundaries on the search path: the same answer (the node's
+    minimum global index, i.e. the workerBits = 0 first hit), found sooner.
+
+    Each rank searches its partition in a thread, window after window (growing from
+    batch_k chunks by `growth` up to batch_candidates_max per window), never waiting for
+    the other ranks.  The calling thread ticks every tick_s: one all-reduce MIN of
+    [best hit, coverage, running] over the node (RCCL over xGMI with the "nccl" backend),
+    where a rank's coverage is the global index below which it has searched all of its
+    candidates (its window frontier, or everything once it holds a hit).  When a best hit
+    is known, every rank lowers the bound of its in-flight search to it (bound_fn ->
+    Miner.bound, dpow_search_bound: the kernel stops claiming work above it at its next
+    group), and the node is done as soon as every rank's coverage reaches the best hit:
+    no rank hashes a whole batch past the answer, and no rank idles at a batch
+    boundary.  Every rank sees the same reduced values, so all take the same decision on
+    the same tick (the all-reduces stay matched).  cancel_fn / clear_fn raise and clear
+    the pinned cancel flag to end the in-flight search at the end.
+
+    The first sync_candidates per rank (2^27: 0.6 ms of hashing) run as node_mine's
+    synchronous batches: a small N ends there without a thread or a tick (the ticked
+    loop costs a few hundred microseconds of latency, which only pays on longer searches).
+
+    search_fn(nonce, ntz, worker_byte, worker_bits, k_begin, k_end, bound) -> SearchResult.
+    """
+    import torch
+    import torch.distributed as dist
+
+    wb, wbits = partition_of_rank(rank, world)
+    rbits = 8 - wbits % 9
+    k_switch = min(k_limit, k_start + (sync_candidates >> rbits))
+    if k_switch > k_start:
+        r = node_mine(search_fn, nonce, num_trailing_zeros, rank, world, batch_k=batch_k, k_start=k_start,
+                      k_limit=k_switch, group=group, device=device, cancelled=cancelled, growth=growth)
+        if r.status != EXHAUSTED or k_switch >= k_limit:
+            return r
+        # continue with windows about the size of the synchronous phase's last batches
+        batch_k = max(batch_k, (k_switch - k_start) >> 1)
+        k_start = k_switch
+    batch_k_max = max(1, batch_candidates_max >> rbits)
+    dist_on = world > 1 and dist.is_available() and dist.is_initialized()
+    if device is None:
+        backend = dist.get_backend(group) if dist_on else "gloo"
+        device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    INF = DPOW_NO_HIT
+    mu = threading.Lock()
+    st = {"best": INF, "secret": None, "cover": k_start << 8, "cancelled": False, "seen": INF, "error": None}
+    stop = threading.Event()
+    changed = threading.Event()  # the searcher's state moved: tick now rather than at the next period
+
+    def searcher():
+        k, bk = k_start, batch_k
+        try:
+            while not stop.is_set():
+                with mu:
+                    bound = min(st["best"], st["seen"])
+                if k >= k_limit or (k << 8) >= bound:  # nothing of ours below the bound is left
+                    with mu:
+                        st["cover"] = INF if (k << 8) >= bound else max(st["cover"], k_limit << 8)
+                    return
+                ke = min(k_limit, k + bk)
+                bk = min(bk * growth, max(bk, batch_k_max))
+                r = search_fn(nonce, num_trailing_zeros, wb, wbits, k, ke, bound)
+                with mu:
+                    if r.status == FOUND:
+                        if r.global_idx < st["best"]:
+                            st["best"], st["secret"] = r.global_idx, r.secret
+                        st["cover"] = INF  # every candidate of ours below our first hit is searched
+                        return
+                    if r.status == CANCELLED:
+                        st["cancelled"] = True
+                        return
+                    st["cover"] = ke << 8
+                changed.set()
+                k = ke
+        except BaseException as e:  # surfaced by the tick loop as a cancel vote + re-raise
+            with mu:
+                st["error"] = e
+                st["cancelled"] = True
+        finally:
+            changed.set()
+
+    th = threading.Thread(target=searcher, daemon=True)
+    th.start()
+    buf = torch.empty(3, dtype=torch.int64, device=device)
+    ticks = 0
+    try:
+        while True:
+            with mu:
+                vals = [st["best"], st["cover"], 0 if (st["cancelled"] or cancelled()) else 1]
+            buf.copy_(torch.tensor(vals, dtype=torch.int64))
+            if dist_on:
+                dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
+            ticks += 1
+            gbest, gcover, grun = (int(x) for x in buf.tolist())
+            if gbest != INF and gcover >= gbest:
+                status = FOUND
+                break
+            if not grun:
+                status = CANCELLED
+                break
+            if gbest == INF and gcover >= (k_limit << 8):
+                status = EXHAUSTED
+                break
+            if gbest != INF:
+                with mu:
+                    lower = gbest < st["seen"]
+                    st["seen"] = min(st["seen"], gbest)
+                if lower:
+                    bound_fn(gbest)  # the in-flight search stops at the node's best hit
+            changed.wait(tick_s)
+            changed.clear()
+    finally:
+        stop.set()
+        cancel_fn()
+        th.join()
+        clear_fn()
+    if st["error"] is not None:
+        raise st["error"]
+    if status != FOUND:
+        return NodeResult(status, batches=ticks)
+    secret = st["secret"] if st["best"] == gbest else None
+    if secret is None:  # another rank's partition won; its owner holds the secret bytes
+        from .search import secret_from_index
+        secret = secret_from_index(gbest)
+    return NodeResult(FOUND, gbest, secret, owner_rank(gbest, world), ticks)

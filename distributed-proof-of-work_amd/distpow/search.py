@@ -138,6 +138,12 @@ class Miner:
     def clear_cancel(self):
         self._cancel[0] = 0
 
+    def bound(self, global_idx: int):
+        """Lower the bound of the search running on this context (from another thread):
+        it stops at global_idx and returns EXHAUSTED unless it has a hit below it
+        (dpow_search_bound).  No effect when no search runs."""
+        check(lib().dpow_search_bound(self._ctx, global_idx), "dpow_search_bound")
+
     @property
     def cancelled(self) -> bool:
         return self._cancel[0] != 0

@@ -89,6 +89,18 @@ int dpow_search(dpow_ctx *ctx, const uint8_t *nonce, size_t nonce_len, uint32_t 
                 uint64_t *best_global_idx, uint8_t secret_out[DPOW_MAX_SECRET],
                 size_t *secret_len);
 
+/* Lower the bound of the search running on ctx, from any thread: candidates at
+ * or above global_idx are no longer wanted (another partition -- another GPU of
+ * the node -- has a hit there).  The running kernel stops claiming work at or
+ * above it within one group of wave-blocks, and dpow_search returns
+ * DPOW_EXHAUSTED unless it finds a hit below the bound (then DPOW_FOUND with
+ * that hit).  Used by the multi-GPU node (distpow.node.node_mine_async) to stop
+ * every rank at the node's best hit without waiting for batch boundaries; the
+ * reference has no counterpart (its coordinator's Found fan-out,
+ * coordinator.go:210-230, cancels instead).  No effect when no search runs.
+ * Returns 0 or a negative error code. */
+int dpow_search_bound(dpow_ctx *ctx, uint64_t global_idx);
+
 /* ---------------------------------------------------------------------------
  * Host helpers (no GPU needed).
  * ------------------------------------------------------------------------- */

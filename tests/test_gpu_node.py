@@ -37,7 +37,7 @@ def _rank_main(rank, world, port, cases, out_q):
     import torch.distributed as dist
 
     import distpow
-    from distpow.node import node_mine
+    from distpow.node import node_mine, node_mine_async
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     res = []
@@ -46,6 +46,12 @@ def _rank_main(rank, world, port, cases, out_q):
         for nonce, ntz in cases:
             r = node_mine(search, nonce, ntz, rank, world, batch_k=1 << 8)
             res.append((r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner, r.batches))
+        # the asynchronous node search: no batch boundaries, the node's best hit injected
+        # into every rank's running search (Miner.bound -> dpow_search_bound)
+        for nonce, ntz in cases:
+            r = node_mine_async(search, nonce, ntz, rank, world, bound_fn=m.bound, cancel_fn=m.cancel,
+                                clear_fn=m.clear_cancel)
+            res.append(("async", r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner))
         # a real cancel on the last rank: its pinned flag stops its kernel mid-launch, the
         # search returns CANCELLED and the all-reduce's running slot stops every rank
         if rank == world - 1:
@@ -82,14 +88,20 @@ def test_node_mine_two_ranks_on_gpu(golden):
             if p.is_alive():
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
+    n = len(cases)
     for rank in range(world):
-        for (nonce, ntz), (status, g, secret, owner, batches) in zip(cases, outs[rank][:-1]):
+        for (nonce, ntz), (status, g, secret, owner, batches) in zip(cases, outs[rank][:n]):
             e = exp[(tuple(nonce), ntz)]
             assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, nonce, ntz, g)
+            assert owner == (g & 0xFF) >> 7
+        for (nonce, ntz), (tag, status, g, secret, owner) in zip(cases, outs[rank][n:2 * n]):
+            e = exp[(tuple(nonce), ntz)]
+            assert tag == "async" and status == 1 and g == e["global_idx"] and secret == e["secret"], \
+                (rank, nonce, ntz, g)
             assert owner == (g & 0xFF) >> 7
         status, batches, secs = outs[rank][-1]
         assert status == 2, outs[rank][-1]  # CANCELLED on every rank
         assert secs < 5
     # the ranks agree batch by batch
-    assert [r[4] for r in outs[0][:-1]] == [r[4] for r in outs[1][:-1]]
+    assert [r[4] for r in outs[0][:n]] == [r[4] for r in outs[1][:n]]
     assert outs[0][-1][1] == outs[1][-1][1]

@@ -405,3 +405,39 @@ def test_n10_min_over_8_partitions(miner, golden):
     assert e9["global_idx"] <= g10
     r9 = miner.search([1, 2, 3, 4], 9, 0, 0, 0, k_stop)
     assert r9.status == FOUND and r9.global_idx == e9["global_idx"]
+
+
+def test_search_bound_from_another_thread(miner, golden):
+    """dpow_search_bound (Miner.bound): a bound injected into the running search stops it
+    at that index.  Below the bound the search's own hit still wins; above it, nothing is
+    wanted and the search returns EXHAUSTED; the bound does not leak into the next search."""
+    e8 = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 8)
+    g8 = e8["global_idx"]  # ~19 ms into the search
+
+    def run_with_bound(ntz, k0, k1, g, delay):
+        out = {}
+        th = threading.Thread(target=lambda: out.update(r=miner.search([1, 2, 3, 4], ntz, 0, 0, k0, k1),
+                                                       t=time.perf_counter()))
+        th.start()
+        time.sleep(delay)
+        t0 = time.perf_counter()
+        miner.bound(g)
+        th.join(timeout=30)
+        assert not th.is_alive()
+        return out["r"], out["t"] - t0
+
+    r, _ = run_with_bound(8, 0, 1 << 32, g8 + 1000, 0.002)   # own hit below the bound: FOUND
+    assert r.status == FOUND and r.global_idx == g8
+    r, _ = run_with_bound(8, 0, 1 << 32, g8 - 1, 0.002)      # the bound is below the hit: nothing wanted
+    assert r.status == EXHAUSTED
+    # unreachable N, bound below the point the search has reached after 0.3 s (~2^28 k):
+    # the running kernel stops at its next group
+    r, lat = run_with_bound(32, 1 << 24, 1 << 40, ((1 << 24) + (1 << 20)) << 8, 0.3)
+    assert r.status == EXHAUSTED and lat < 0.25, lat
+    print(f"bound -> return {lat * 1e3:.2f} ms")
+    e6 = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 6)
+    r = miner.search([1, 2, 3, 4], 6, 0, 0, 0, 1 << 30)
+    assert r.status == FOUND and r.global_idx == e6["global_idx"]
+    miner.bound(5)  # no search in flight: no effect
+    r = miner.search([1, 2, 3, 4], 6, 0, 0, 0, 1 << 30)
+    assert r.status == FOUND and r.global_idx == e6["global_idx"]

@@ -34,6 +34,59 @@ def _oracle_search_fn():
     return fn
 
 
+def _worker_async(rank, world, port, cases, out_q, cancel_rank):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+    import torch.distributed as dist
+    from distpow.node import node_mine_async
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    fn = _oracle_search_fn()
+    res = []
+    for sync in (0, 1 << 12):  # purely ticked; and a synchronous first phase handing over to it
+        for nonce, ntz in cases:
+            r = node_mine_async(fn, nonce, ntz, rank, world, batch_k=64, batch_candidates_max=1 << 16,
+                                sync_candidates=sync)
+            res.append((r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner))
+    # a window with no hit: every rank exhausts k_limit
+    r = node_mine_async(fn, [1, 2, 3, 4], 32, rank, world, batch_k=16, k_limit=1 << 12, sync_candidates=0)
+    res.append((r.status,))
+    # cancellation vote: one rank reports cancelled -> every rank stops
+    r = node_mine_async(fn, [1, 2, 3, 4], 32, rank, world, batch_k=16, k_limit=1 << 20,
+                        cancelled=(lambda: rank == cancel_rank), sync_candidates=0)
+    res.append((r.status,))
+    out_q.put((rank, res))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_node_mine_async_gloo_matches_wbits0_answer(golden, world):
+    """node_mine_async: ranks search without batch boundaries and tick an all-reduce of
+    [best, coverage, running]; the answer is still the workerBits = 0 golden."""
+    cases = [(e["nonce"], e["ntz"]) for e in golden["first_hits"] if e["global_idx"] < 200_000]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_async, args=(r, world, port, cases, q, world - 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = {(tuple(e["nonce"]), e["ntz"]): e for e in golden["first_hits"]}
+    for rank in range(world):
+        res = outs[rank]
+        assert len(res) == 2 * len(cases) + 2
+        for (nonce, ntz), (status, g, secret, owner) in zip(cases + cases, res[:-2]):
+            e = exp[(tuple(nonce), ntz)]
+            assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, nonce, ntz)
+            assert owner == (g & 0xFF) >> (8 - (world.bit_length() - 1))
+        assert res[-2] == (0,)  # EXHAUSTED
+        assert res[-1] == (2,)  # CANCELLED
+
+
 def _worker(rank, world, port, cases, out_q, cancel_rank):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))

@@ -257,6 +257,7 @@ def main():
             **extra,
             "cpu_baseline": cpu,
             "geometry": {"cus": cus, "threads_per_block": tpb},
+            "build_id": distpow.build_id(),  # = the sources' hash (distpow._lib.check_build refused anything else)
         }
         print(json.dumps(out), flush=True)
     miner.close()

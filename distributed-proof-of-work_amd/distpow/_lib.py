@@ -98,7 +98,10 @@ def _rebuild():
         fcntl.flock(lk, fcntl.LOCK_EX)
         print(f"distpow: libdpow.so does not match the sources; rebuilding (make -j{jobs})",
               file=sys.stderr, flush=True)
-        subprocess.check_call(["make", "-s", "-j", jobs, "-C", CSRC], stdout=sys.stderr)
+        # output captured (sys.stderr may be a pytest capture object without a file descriptor)
+        r = subprocess.run(["make", "-s", "-j", jobs, "-C", CSRC], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise ImportError(f"rebuilding libdpow.so failed:\n{(r.stdout + r.stderr)[-4000:]}")
     return True
 
 

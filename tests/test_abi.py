@@ -77,3 +77,31 @@ def test_library_build_id_matches_sources():
     assert distpow.build_id() == want
     assert _lib.library_build_id() == want
     assert len(want) == 16 and int(want, 16) >= 0
+
+
+def _build_c_harness(tmp_path):
+    import distpow
+    exe = str(tmp_path / "abi_harness")
+    libdir = os.path.dirname(distpow.LIB_PATH)
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-pedantic",
+                           "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c", "abi_harness.c"),
+                           "-L", libdir, "-ldpow", f"-Wl,-rpath,{libdir}", "-o", exe])
+    return exe
+
+
+def test_c_abi_from_plain_c(tmp_path):
+    """The headers are plain C11 (cgo compiles its preamble as C) and libdpow.so links and
+    runs from a C program: host entry points, argument checks, struct layout."""
+    import json
+    import distpow
+    distpow.lib()  # the build-id check
+    out = subprocess.check_output([_build_c_harness(tmp_path)], timeout=60).decode()
+    rec = json.loads(out)
+    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 1
+
+
+@pytest.mark.gpu
+def test_c_abi_search_from_plain_c(tmp_path):
+    import json
+    out = subprocess.check_output([_build_c_harness(tmp_path), "gpu"], timeout=120).decode()
+    assert json.loads(out)["search"] == 2532284

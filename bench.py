@@ -201,10 +201,18 @@ def main():
     # (FETCH_SIZE and WRITE_SIZE in separate passes, tools/profile_gpu.sh + tools/summarize_profile.py),
     # uncorrected: the search reads no data, so these bytes are kernarg scalar loads, the claim
     # atomics and the completion records -- not algorithmic HBM traffic (that is 0 per candidate).
-    traffic, traffic_src = None, None
+    traffic, traffic_src, issue = None, None, None
     prof = os.path.join(ROOT, "profiles", PROFILE_TAG + "_summary.json")
     if os.path.exists(prof):
         ps = json.load(open(prof))
+        if "valu_busy_issue_model" in ps:
+            # SQ_INSTS_VALU per SIMD-cycle weighted by the hash block's mix (2 cycles per
+            # full-rate, 4 per half-rate wave64 instruction): ~1.0 = the SIMDs issue VALU
+            # every cycle; the gap from frac to 1 is gfx950's half-rate add3 / alignbit
+            issue = {"valu_busy": round(ps["valu_busy_issue_model"], 4),
+                     "valu_insts_per_candidate": round(ps["valu_insts_per_candidate"], 2),
+                     "clock_ghz": round(ps["effective_clock_ghz"], 3),
+                     "source": f"profiles/{PROFILE_TAG}_summary.json (rocprofv3 SQ/GRBM pass)"}
         if "hbm_bytes_per_launch" in ps:
             traffic = int(ps["hbm_bytes_per_launch"])
             traffic_src = (f"profiles/{PROFILE_TAG}_summary.json: FETCH_SIZE + WRITE_SIZE per "
@@ -247,6 +255,7 @@ def main():
                 "avg_launch_ms": round(avg_launch_ms, 4),
                 "candidates_per_launch": int(cand_per_launch),
                 "launches": int(st.launches),
+                "issue": issue,
             },
             "stream_event_ms": round(stream_ms, 3),
             "valu_probe": probe,

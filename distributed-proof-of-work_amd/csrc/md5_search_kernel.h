@@ -7,7 +7,8 @@
 // an unrolled, register-resident MD5 of the final message block(s) of two
 // candidates, software-pipelined in hand-ordered asm groups (see pipe::), the
 // message words being wave-uniform (kernel arguments, SGPRs) except the 4 bytes
-// threadByte | k_lo << 8.
+// threadByte | k_lo << 8, and the bytes of k >> 24 (L >= 4), which change once
+// per 2^24-k segment of a launch (the segment words, re-derived per wave).
 //
 // Work decomposition: local index i = k * R + t (the reference's order, k outer,
 // t inner).  A wave-block is 64 * kNC consecutive indices (lane l, slot j ->

@@ -103,7 +103,7 @@ class Miner:
     and the pinned cancel flag that Found/Cancel raise (worker.go:194,209)."""
 
     # k-window per dpow_search call.  Launches inside a window are queued
-    # back-to-back (split at chunk-length and 2^24-k boundaries); a call returns
+    # back-to-back (split where the chunk length changes); a call returns
     # at the first window holding a hit.
     DEFAULT_WINDOW = 1 << 26
 

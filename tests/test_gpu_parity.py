@@ -441,3 +441,37 @@ def test_search_bound_from_another_thread(miner, golden):
     miner.bound(5)  # no search in flight: no effect
     r = miner.search([1, 2, 3, 4], 6, 0, 0, 0, 1 << 30)
     assert r.status == FOUND and r.global_idx == e6["global_idx"]
+
+
+def test_concurrent_searches_share_the_gpu(golden):
+    """Four contexts searching at once on one GPU (each sizes its grids to its share of the
+    device, dpow_api.cpp ActiveSearch): every answer is still the golden, and a concurrent
+    unreachable search is cancelled without disturbing the others."""
+    cases = [([1, 2, 3, 4], 7), ([2, 2, 2, 2], 8), ([5, 6, 7, 8], 5), ([1, 2, 3, 4], 8)]
+    exp = {(tuple(e["nonce"]), e["ntz"]): e for e in golden["first_hits"]}
+    miners = [distpow.Miner(0) for _ in range(len(cases) + 1)]
+    out = {}
+    try:
+        def run(i, nonce, ntz):
+            out[i] = miners[i].mine(nonce, ntz)
+
+        def run_forever():
+            out["inf"] = miners[-1].search([9, 9, 9, 9], 32, 0, 0, 1 << 24, 1 << 40)
+
+        ths = [threading.Thread(target=run, args=(i, n, z)) for i, (n, z) in enumerate(cases)]
+        ths.append(threading.Thread(target=run_forever))
+        for t in ths:
+            t.start()
+        for t in ths[:-1]:
+            t.join(timeout=60)
+        miners[-1].cancel()
+        ths[-1].join(timeout=30)
+        miners[-1].clear_cancel()
+        assert not any(t.is_alive() for t in ths)
+        for i, (nonce, ntz) in enumerate(cases):
+            e = exp[(tuple(nonce), ntz)]
+            assert out[i].status == FOUND and (out[i].global_idx, list(out[i].secret)) == (e["global_idx"], e["secret"])
+        assert out["inf"].status == CANCELLED
+    finally:
+        for m in miners:
+            m.close()

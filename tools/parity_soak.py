@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
 """Randomised parity soak of the GPU search against the C oracle (test infrastructure).
 
-    python tools/parity_soak.py [seconds] [seed]
+    python tools/parity_soak.py [seconds] [seed] [span]
 
 Random nonce lengths (0..130, every kernel layout), partitions (workerBits 0..10),
 windows (every chunk-length segment, straddling segment / 2^24 boundaries) and
 trailing-zero counts (1..5); every GPU answer must equal the oracle's first hit
 (or "no hit").  Prints one JSON line with the case count (progress on stderr every
 30 s).  GPU box only.
+
+With "span" every case is a window across one or more 2^24-k segment boundaries
+(the segment-word path of launches that span segments): workerBits 5..8 (8..1
+thread bytes per k), up to ~2^20 candidates, L = 4 and 5.
 """
 import json
 import os
@@ -24,6 +28,7 @@ from _oracle import Oracle  # noqa: E402
 
 secs = float(sys.argv[1]) if len(sys.argv) > 1 else 60.0
 seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+span = len(sys.argv) > 3 and sys.argv[3] == "span"
 rnd = random.Random(seed)
 o = Oracle()
 n_cases = hits = 0
@@ -44,6 +49,16 @@ with distpow.Miner(0) as m:
         if seg >= 4 and rnd.random() < 0.3:
             k0 = max(0, ((k0 >> 24) + 1 << 24) - rnd.randrange(1, 64))
         nk = max(1, rnd.randrange(1, 1 + (1 << 17) // (1 << rb)))
+        if span:  # straddle 1..3 segment boundaries of L = 4 or 5
+            wbits = rnd.choice([5, 6, 7, 8])
+            wb = rnd.randrange(1 << wbits)
+            rb = 8 - wbits
+            edge = rnd.choice([rnd.randrange(2, 255), rnd.randrange(257, 1 << 16)]) << 24
+            nk = rnd.randrange(2, (1 << 20) >> rb)
+            k0 = edge - rnd.randrange(1, nk)
+            if rnd.random() < 0.3:  # a window over whole segments
+                nk += rnd.randrange(1, 3) << 24 if rb == 0 else 0
+            ntz = rnd.choice([3, 4, 4, 5, 5])
         k1 = min(k0 + nk, 1 << 40)
         exp = o.mine_window(nonce, ntz, wb, wbits, k0, k1)
         r = m.search(nonce, ntz, wb, wbits, k0, k1)
@@ -57,4 +72,4 @@ with distpow.Miner(0) as m:
         if time.time() >= t_log:  # progress line: a silent run looks hung to the GPU harness
             print(f"... {n_cases} cases, {hits} hits", file=sys.stderr, flush=True)
             t_log += 30
-print(json.dumps({"cases": n_cases, "hits": hits, "seed": seed, "seconds": secs}))
+print(json.dumps({"cases": n_cases, "hits": hits, "seed": seed, "seconds": secs, "span": span}))

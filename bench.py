@@ -82,9 +82,12 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     device = 0 if args.same_device else local_rank
     torch.cuda.set_device(device)
+    tick_group = None
     if world > 1:
         if args.backend == "nccl":  # RCCL over xGMI
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            if not NODE_SYNC:  # node_mine_async's ticks: a host (gloo) group, off the busy GPUs
+                tick_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group("gloo")
     wb, wbits = partition_of_rank(rank, world)
@@ -162,7 +165,7 @@ def main():
             else:  # no batch boundaries: ticked all-reduce + the node's best injected into each rank's search
                 res = node_mine_async(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
                                       bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
-                                      batch_k=TTS_BATCH_K, device=dev)
+                                      batch_k=TTS_BATCH_K, device=dev, tick_group=tick_group)
             barrier()
             runs.append((time.perf_counter() - t1) * 1e3)
             assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)

@@ -114,7 +114,7 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
                     k_limit: int = DPOW_K_LIMIT, group=None, device=None,
                     cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
                     batch_candidates_max: int = 1 << 31, tick_s: float = 1e-4,
-                    sync_candidates: int = 1 << 27) -> NodeResult:
+                    sync_candidates: int = 1 << 27, tick_group=None, tick_device=None) -> NodeResult:
     """node_mine without batch boundaries on the search path: the same answer (the node's
     minimum global index, i.e. the workerBits = 0 first hit), found sooner.
 
@@ -135,6 +135,10 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
     The first sync_candidates per rank (2^27: 0.6 ms of hashing) run as node_mine's
     synchronous batches: a small N ends there without a thread or a tick (the ticked
     loop costs a few hundred microseconds of latency, which only pays on longer searches).
+
+    tick_group / tick_device: where the ticks' all-reduce runs (default: group / device).
+    With the nccl backend a gloo group on the host keeps the 24-byte control message off
+    the GPUs, whose CUs the persistent search grids occupy while the ticks run.
 
     search_fn(nonce, ntz, worker_byte, worker_bits, k_begin, k_end, bound) -> SearchResult.
     """
@@ -157,6 +161,13 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
     if device is None:
         backend = dist.get_backend(group) if dist_on else "gloo"
         device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    if tick_group is None:
+        tick_group = group
+    if tick_device is None:
+        if tick_group is not None and dist_on:
+            tick_device = torch.device("cpu") if dist.get_backend(tick_group) == "gloo" else device
+        else:
+            tick_device = device
     INF = DPOW_NO_HIT
     mu = threading.Lock()
     st = {"best": INF, "secret": None, "cover": k_start << 8, "cancelled": False, "seen": INF, "error": None}
@@ -197,7 +208,7 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
 
     th = threading.Thread(target=searcher, daemon=True)
     th.start()
-    buf = torch.empty(3, dtype=torch.int64, device=device)
+    buf = torch.empty(3, dtype=torch.int64, device=tick_device)
     ticks = 0
     try:
         while True:
@@ -205,7 +216,7 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
                 vals = [st["best"], st["cover"], 0 if (st["cancelled"] or cancelled()) else 1]
             buf.copy_(torch.tensor(vals, dtype=torch.int64))
             if dist_on:
-                dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
+                dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=tick_group)
             ticks += 1
             gbest, gcover, grun = (int(x) for x in buf.tolist())
             if gbest != INF and gcover >= gbest:

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Correctness sweep over every message layout (GPU box only): for nonce lengths
+"""Correctness sweep over every message layout (GPU box only; test infrastructure under
+tests/ because it loads the oracle, not collected by pytest): for nonce lengths
 0..130 (every (NBLK, W0, SH) layout, midstate and two-block cases), search windows in
 every chunk-length segment at N = 1..3 and compare with the byte-wise oracle; prints
 the failing (length, layout, window) cases, exit 1 if any.  Quicker to localise a
@@ -9,7 +10,7 @@ import os
 import random
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "distributed-proof-of-work_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: F401,E402

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Randomised parity soak of the GPU search against the C oracle (test infrastructure).
+"""Randomised parity soak of the GPU search against the C oracle (test infrastructure:
+lives under tests/ because it loads the oracle; not collected by pytest).
 
-    python tools/parity_soak.py [seconds] [seed] [span]
+    python tests/soak/parity_soak.py [seconds] [seed] [span]
 
 Random nonce lengths (0..130, every kernel layout), partitions (workerBits 0..10),
 windows (every chunk-length segment, straddling segment / 2^24 boundaries) and
@@ -19,7 +20,7 @@ import random
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "distributed-proof-of-work_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: F401,E402

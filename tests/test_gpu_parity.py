@@ -414,7 +414,7 @@ def test_search_bound_from_another_thread(miner, golden):
     e8 = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 8)
     g8 = e8["global_idx"]  # ~19 ms into the search
 
-    def run_with_bound(ntz, k0, k1, g, delay):
+    def run_with_bound(ntz, k0, k1, g, delay, repeat=False):
         out = {}
         th = threading.Thread(target=lambda: out.update(r=miner.search([1, 2, 3, 4], ntz, 0, 0, k0, k1),
                                                        t=time.perf_counter()))
@@ -422,13 +422,18 @@ def test_search_bound_from_another_thread(miner, golden):
         time.sleep(delay)
         t0 = time.perf_counter()
         miner.bound(g)
+        # a bound that lands before the thread's search has opened applies to nothing
+        # (dpow_search_bound: no search in flight): repeat it until the search returns
+        while repeat and th.is_alive():
+            time.sleep(0.001)
+            miner.bound(g)
         th.join(timeout=30)
         assert not th.is_alive()
         return out["r"], out["t"] - t0
 
-    r, _ = run_with_bound(8, 0, 1 << 32, g8 + 1000, 0.002)   # own hit below the bound: FOUND
+    r, _ = run_with_bound(8, 0, 1 << 32, g8 + 1000, 0.002, repeat=True)  # own hit below the bound: FOUND
     assert r.status == FOUND and r.global_idx == g8
-    r, _ = run_with_bound(8, 0, 1 << 32, g8 - 1, 0.002)      # the bound is below the hit: nothing wanted
+    r, _ = run_with_bound(8, 0, 1 << 32, g8 - 1, 0.002, repeat=True)     # the bound is below the hit: nothing wanted
     assert r.status == EXHAUSTED
     # unreachable N, bound below the point the search has reached after 0.3 s (~2^28 k):
     # the running kernel stops at its next group

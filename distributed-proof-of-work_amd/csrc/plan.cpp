@@ -4,14 +4,15 @@
 //   for k = 0, 1, ... (chunk_k = nextChunk^k([]), worker.go:234-244, 399)
 //     for t in 0..R-1: msg = nonce || threadByte[t] || chunk_k   (worker.go:319-353)
 // A launch covers a k-range in which the chunk length L is constant (segment
-// boundaries k = 1, 2^8, 2^16, 2^24, 2^32), so the message layout is uniform.
+// boundaries k = 1, 2^8, 2^16, ..., 2^48), so the message layout is uniform.
 // The per-candidate bytes are V = threadByte | (k mod 2^24) << 8, at byte
 // offset p = nonce_len mod 64 of the first final block, and for L >= 4 the
 // bytes of k >> 24 at p + 4, which change once every 2^24 k: the template
 // holds the launch's first value (Launch::seg_first) and the kernel re-derives
 // the K + M constants of the word(s) holding them when a wave moves into
-// another 2^24-k segment.  Whole nonce-only blocks before p are hashed here
-// once (midstate).
+// another 2^24-k segment.  For SH = 1-2 and L >= 6 the top chunk bytes reach
+// word W0 + 2, which the kernel holds launch-uniform (word2_period).  Whole
+// nonce-only blocks before p are hashed here once (midstate).
 #include "plan.h"
 
 #include <string.h>
@@ -33,6 +34,13 @@ uint64_t segment_end(uint64_t k) {
     return 1ull << (8 * L);
 }
 
+uint64_t word2_period(uint32_t sh) {
+    // k >> 24 sits at byte SH of the 64-bit pair (W0 + 1, W0 + 2): its bits from
+    // 32 - 8 SH on land in W0 + 2.  SH = 3's W0 + 2 is a kernel segment word; for
+    // SH = 0 nothing reaches W0 + 2 below DPOW_K_LIMIT.
+    return (sh == 1 || sh == 2) ? 1ull << (56 - 8 * sh) : 0;
+}
+
 uint32_t remainder_bits(uint32_t worker_bits) { return 8u - (worker_bits % 9u); }
 
 uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits) {
@@ -44,7 +52,7 @@ int WindowPlanner::init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, ui
                         uint32_t worker_bits, uint64_t k_begin, uint64_t k_end) {
     if (nonce_len && !nonce) return -1;
     if (worker_byte > 255u) return -1;
-    if (k_end > (1ull << 40)) return -4;
+    if (k_end > DPOW_K_LIMIT) return DPOW_ERANGE;
     nonce_ = nonce;
     nonce_len_ = nonce_len;
     ntz_ = ntz;
@@ -67,7 +75,11 @@ int WindowPlanner::init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, ui
 bool WindowPlanner::next(PlannedLaunch &pl) {
     if (k_ >= k_end_) return false;
     const uint64_t k = k_;
-    const uint64_t ke = segment_end(k) < k_end_ ? segment_end(k) : k_end_;
+    uint64_t ke = segment_end(k) < k_end_ ? segment_end(k) : k_end_;
+    if (const uint64_t w2 = word2_period(p_ % 4)) {  // word W0 + 2 changes: end the launch
+        const uint64_t we = (k / w2 + 1) * w2;
+        if (we < ke) ke = we;
+    }
     const uint32_t L = chunk_len_of(k);
     const size_t msg_len = nonce_len_ + 1 + L;
     const size_t total_blocks = (msg_len + 8) / 64 + 1;

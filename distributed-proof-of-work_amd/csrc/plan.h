@@ -17,6 +17,9 @@ struct PlannedLaunch {
 
 uint32_t chunk_len_of(uint64_t k);
 uint64_t segment_end(uint64_t k);
+// k-period of word W0 + 2's chunk bytes for byte shift SH (0: launch-uniform
+// or a kernel segment word); the planner ends launches on its multiples.
+uint64_t word2_period(uint32_t sh);
 uint32_t remainder_bits(uint32_t worker_bits);
 uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits);
 

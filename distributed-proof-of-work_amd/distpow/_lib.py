@@ -24,7 +24,7 @@ LIB_PATH = LIB_OVERRIDE or os.path.join(_HERE, "libdpow.so")
 
 DPOW_NO_HIT = 0x7FFFFFFFFFFFFFFF
 DPOW_MAX_SECRET = 16
-DPOW_K_LIMIT = 1 << 40
+DPOW_K_LIMIT = (1 << 55) - 1  # include/dpow.h: chunks of up to 7 bytes, every index < DPOW_NO_HIT
 EXHAUSTED, FOUND, CANCELLED = 0, 1, 2
 EINVAL, EHIP, EVERIFY, ERANGE, ENOMEM = -1, -2, -3, -4, -5
 

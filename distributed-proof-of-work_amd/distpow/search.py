@@ -164,7 +164,7 @@ class Miner:
     def mine(self, nonce: Sequence[int], num_trailing_zeros: int, worker_byte: int = 0, worker_bits: int = 0,
              k_start: int = 0, k_limit: int = DPOW_K_LIMIT, window: int = DEFAULT_WINDOW) -> SearchResult:
         """worker.go:318-400: search k = k_start, k_start + 1, ... until a hit, the
-        cancel flag, or k_limit (the reference has no limit; DPOW_K_LIMIT = 2^40 k)."""
+        cancel flag, or k_limit (the reference has no limit; DPOW_K_LIMIT = 2^55 - 1 k)."""
         k = k_start
         while k < k_limit:
             ke = min(k_limit, k + window)

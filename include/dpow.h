@@ -30,13 +30,15 @@ extern "C" {
  * int64 MIN) and unsigned (device atomicMin u64) reductions agree. */
 #define DPOW_NO_HIT 0x7FFFFFFFFFFFFFFFull
 
-/* Longest secret the search can return: 1 thread byte + 5 chunk bytes
- * (k < 2^40).  Buffers are sized 16 for headroom. */
+/* Longest secret the search can return: 1 thread byte + 7 chunk bytes
+ * (k < DPOW_K_LIMIT).  Buffers are sized 16 for headroom. */
 #define DPOW_MAX_SECRET 16
 
 /* k (the number of nextChunk applications, worker.go:234-244/399) is limited to
- * k < DPOW_K_LIMIT, i.e. chunks of at most 5 bytes (2^48 candidates). */
-#define DPOW_K_LIMIT (1ull << 40)
+ * k < DPOW_K_LIMIT = 2^55 - 1: chunks of at most 7 bytes, and every global index
+ * k * 256 + threadByte stays below DPOW_NO_HIT (about 2^63 candidates: decades of
+ * a GPU node, so the reference's unbounded loop is never cut short in practice). */
+#define DPOW_K_LIMIT ((1ull << 55) - 1)
 
 /* dpow_search return codes */
 #define DPOW_EXHAUSTED 0   /* window searched, no hit (the reference keeps looping) */

@@ -76,13 +76,52 @@ def test_random_windows_vs_oracle(miner, oracle):
 
 
 def test_top_of_k_range(miner, oracle):
-    k0 = (1 << 40) - 2048
-    for ntz in (1, 2, 3):
-        exp = oracle.mine_window([9, 8, 7, 6], ntz, 0, 0, k0, 1 << 40)
-        r = miner.search([9, 8, 7, 6], ntz, 0, 0, k0, 1 << 40)
-        assert r.status == FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1])
+    """The chunk-length boundaries 2^40 / 2^48 (6- and 7-byte chunks) and the last k
+    before DPOW_K_LIMIT = 2^55 - 1 (7-byte secrets whose global index k * 256 + t stays
+    below DPOW_NO_HIT); a window past the limit is an error, not a wrapped index."""
+    top = distpow.DPOW_K_LIMIT
+    for k0, k1 in (((1 << 40) - 2048, 1 << 40), ((1 << 40) - 700, (1 << 40) + 700),
+                   ((1 << 48) - 700, (1 << 48) + 700), (top - 2048, top)):
+        for ntz in (1, 2, 3):
+            exp = oracle.mine_window([9, 8, 7, 6], ntz, 0, 0, k0, k1)
+            r = miner.search([9, 8, 7, 6], ntz, 0, 0, k0, k1)
+            assert r.status == FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1]), (k0, ntz)
+    # every thread byte of the last k (workerBits 0: the largest global indices there are)
+    exp = oracle.mine_window([9, 8, 7, 6], 1, 0, 0, top - 1, top)
+    r = miner.search([9, 8, 7, 6], 1, 0, 0, top - 1, top)
+    assert (r.status, r.global_idx) == ((FOUND, exp[1]) if exp else (EXHAUSTED, DPOW_NO_HIT))
+    if exp:
+        assert list(r.secret) == exp[0] and len(r.secret) == 8  # thread byte + 7 chunk bytes
     with pytest.raises(distpow.DpowError):
-        miner.search([1], 1, 0, 0, 0, (1 << 40) + 1)
+        miner.search([1], 1, 0, 0, 0, top + 1)
+
+
+def test_long_chunks_vs_oracle(miner, oracle):
+    """6- and 7-byte chunks (k in [2^40, 2^55 - 1)) for every byte shift and both block
+    counts, random partitions, windows at and across the launch splits the planner puts
+    there (2^24-k segments, word W0+2's period for SH 1-2, 2^48), oracle-sized."""
+    rnd = random.Random(4855)
+    top = distpow.DPOW_K_LIMIT
+    for it in range(120):
+        nlen = rnd.choice([0, 1, 2, 3, 4, 5, 6, 7, 13, 46, 47, 48, 49, 50, 52, 55, 57, 59, 60, 61, 62, 63, 64, 66])
+        nonce = [rnd.randrange(256) for _ in range(nlen)]
+        wbits = rnd.choice([0, 0, 2, 3, 6, 8])
+        wb = rnd.randrange(1 << (wbits % 9)) if wbits % 9 else rnd.randrange(256)
+        rb = 8 - wbits % 9
+        ntz = rnd.choice([1, 2, 3, 3, 4])
+        edge = rnd.choice([1 << 40, 1 << 48, rnd.randrange(1 << 40, 1 << 48) >> 24 << 24,
+                           rnd.randrange(1 << 48, top) >> 24 << 24, rnd.randrange(2, 255) << 40,
+                           rnd.randrange(2, 127) << 48, rnd.randrange(1 << 40, top)])
+        nk = max(1, rnd.randrange(1, 1 + (1 << 16) // (1 << rb)))
+        k0 = max(1 << 40, edge - rnd.randrange(0, nk + 1))
+        k1 = min(k0 + nk, top)
+        exp = oracle.mine_window(nonce, ntz, wb, wbits, k0, k1)
+        r = miner.search(nonce, ntz, wb, wbits, k0, k1)
+        if exp is None:
+            assert r.status == EXHAUSTED, (it, nlen, ntz, wb, wbits, k0, k1, r)
+        else:
+            assert r.status == FOUND and r.global_idx == exp[1] and list(r.secret) == exp[0], \
+                (it, nlen, ntz, wb, wbits, k0, k1, r, exp)
 
 
 def test_empty_window_and_unreachable(miner):
@@ -331,6 +370,15 @@ def _all_hits(miner, nonce, ntz, wb, wbits, k0, k1, cap=2000):
     (8, (1 << 32) + (3 << 24) - 5, 6),         # L = 5, SH 0
     (60, (1 << 24) + 3, 6),                    # two final blocks, W0 = 15: the segment word is block 1's word 0
     (63, (1 << 32) + (254 << 24), 5),          # two final blocks, SH 3, L = 5: words 16 and 17
+    # chunks of 6 and 7 bytes (k >= 2^40; DPOW_K_LIMIT = 2^55 - 1)
+    (4, (1 << 40) + (0xFE << 32) + (250 << 24) + 5, 10),      # SH 0, L = 6: k >> 24 carries over two bytes
+    (5, (7 << 40) + (0xFFFF << 24) - 3, 6),                   # SH 1, L = 6: three bytes in word W0+1
+    (6, (5 << 40) - (3 << 24) - 7, 6),                        # SH 2, L = 6: word W0+2 changes at 5 * 2^40
+    (7, (3 << 48) + (0x12 << 40) + (0xFF << 32) + (0xFD << 24) + 11, 6),  # SH 3, L = 7: W0+1 -> W0+2 carry
+    (5, (9 << 48) - (2 << 24) - 1, 5),                        # SH 1, L = 7: word W0+2 changes at 9 * 2^48
+    (60, (1 << 50) + (0xFF << 24) + 9, 5),                    # two blocks, W0 = 15, SH 0, L = 7
+    (62, (2 << 40) - (2 << 24) + 1, 5),                       # two blocks, SH 2, L = 6, across 2 * 2^40
+    (4, (1 << 55) - 1 - (3 << 24) - 100, 3),                  # the top of the k range
 ])
 def test_spanning_launch_equals_per_segment_windows(miner, oracle, nlen, first_k, nseg):
     """The segment-word path (DPOW_SPAN): one search over a window spanning nseg 2^24-k

@@ -66,9 +66,28 @@ def test_plan_window_segments():
     pl = distpow.plan_window(b"ab", 0, 0, (1 << 32) - 9, (1 << 32) + 2 * (1 << 24))
     assert [(p.k_begin, p.k_end, p.chunk_len) for p in pl] == [((1 << 32) - 9, 1 << 32, 4),
                                                                (1 << 32, (1 << 32) + (2 << 24), 5)]
+    # L = 6 / 7 (k >= 2^40): for SH = 1-2 the top chunk bytes reach word W0 + 2, which
+    # the kernel holds launch-uniform, so launches also end where it changes (every
+    # 2^40 k for SH = 2, 2^48 for SH = 1); SH = 0 / 3 windows split only at chunk lengths
+    w = ((3 << 40) - 5, (4 << 40) + 9)
+    assert [(p.k_begin, p.k_end) for p in distpow.plan_window(b"ab", 0, 0, *w)] == \
+        [((3 << 40) - 5, 3 << 40), (3 << 40, (4 << 40)), (4 << 40, (4 << 40) + 9)]  # SH = 2
+    assert [(p.k_begin, p.k_end) for p in distpow.plan_window(b"abc", 0, 0, *w)] == [w]  # SH = 3
+    assert [(p.k_begin, p.k_end) for p in distpow.plan_window(b"abcd", 0, 0, *w)] == [w]  # SH = 0
+    assert [(p.k_begin, p.k_end) for p in distpow.plan_window(b"a", 0, 0, *w)] == [w]  # SH = 1: 2^48
+    w = ((2 << 48) - 3, (2 << 48) + 3)
+    assert [(p.k_begin, p.k_end, p.chunk_len) for p in distpow.plan_window(b"a", 0, 0, *w)] == \
+        [((2 << 48) - 3, 2 << 48, 7), (2 << 48, (2 << 48) + 3, 7)]
+    assert len(distpow.plan_window(b"abc", 0, 0, *w)) == 1
+    # the top of the k range: k < DPOW_K_LIMIT = 2^55 - 1, so every global index
+    # k * 256 + t is below DPOW_NO_HIT = 2^63 - 1
+    assert distpow.DPOW_K_LIMIT == (1 << 55) - 1
+    assert ((distpow.DPOW_K_LIMIT - 1) << 8 | 255) < distpow.DPOW_NO_HIT
+    pl = distpow.plan_window(b"x", 0, 0, distpow.DPOW_K_LIMIT - 4, distpow.DPOW_K_LIMIT)
+    assert [(p.k_begin, p.k_end, p.chunk_len) for p in pl] == [(distpow.DPOW_K_LIMIT - 4, distpow.DPOW_K_LIMIT, 7)]
     # beyond the k limit
     with pytest.raises(distpow.DpowError):
-        distpow.plan_window(b"x", 0, 0, 0, (1 << 40) + 1)
+        distpow.plan_window(b"x", 0, 0, 0, distpow.DPOW_K_LIMIT + 1)
 
 
 def _expected_words(nonce: bytes, secret: bytes):
@@ -110,7 +129,8 @@ def test_candidate_words_every_layout(nlen):
     for wb, wbits in [(0, 0), (1, 2), (6, 3), (3, 8), (2, 1), (5, 9)]:
         rb = 8 - wbits % 9
         for k in (0, 1, 200, 255, 256, 4097, 65535, 65536, 1 << 20, (1 << 24) - 1, 1 << 24,
-                  (1 << 24) + 77, (1 << 32) - 1, 1 << 32, (1 << 33) + 12345, (1 << 40) - 1):
+                  (1 << 24) + 77, (1 << 32) - 1, 1 << 32, (1 << 33) + 12345, (1 << 40) - 1, 1 << 40,
+                  (5 << 40) + 99, (1 << 48) - 1, 1 << 48, (0x3456 << 40) + 7, (1 << 55) - 2):
             for t in {0, (1 << rb) - 1, rnd.randrange(1 << rb)}:
                 _check_candidate(nonce, wb, wbits, (k << rb) | t)
 
@@ -124,5 +144,6 @@ def test_candidate_words_random_lanes():
         wb = rnd.randrange(256) if wbits in (0, 9) else rnd.randrange(1 << (wbits % 9) if wbits % 9 else 1)
         rb = 8 - wbits % 9
         k = rnd.choice([rnd.randrange(1 << 8), rnd.randrange(1 << 16), rnd.randrange(1 << 24),
-                        rnd.randrange(1 << 32), rnd.randrange(1 << 40)])
+                        rnd.randrange(1 << 32), rnd.randrange(1 << 40), rnd.randrange(1 << 48),
+                        rnd.randrange((1 << 55) - 1)])
         _check_candidate(nonce, wb, wbits, (k << rb) | rnd.randrange(1 << rb))

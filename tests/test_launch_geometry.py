@@ -72,11 +72,14 @@ def test_boundary_straddling_windows(max_blocks):
         wbits = rnd.choice([0, 1, 2, 3, 5, 8, 9, 10])
         wb = rnd.randrange(1 << (wbits % 9)) if wbits % 9 else 0
         m = rnd.randrange(1, 300)
-        if rnd.random() < 0.5:
+        u = rnd.random()
+        if u < 0.4:
             m += 256  # k >= 2^32 too (L = 5)
+        elif u < 0.6:
+            m += rnd.choice([1 << 16, 1 << 24, rnd.randrange(1 << 16, 1 << 31)])  # L = 6 / 7
         edge = m << 24
         k0 = max(1 << 24, edge - rnd.randrange(1, 3000))
-        k1 = min(1 << 40, edge + rnd.randrange(1, 3000))
+        k1 = min(distpow.DPOW_K_LIMIT, edge + rnd.randrange(1, 3000))
         nonce = [rnd.randrange(256) for _ in range(rnd.choice([0, 3, 4, 7, 55, 60, 64]))]
         for d in geometry(nonce, wb, wbits, k0, k1, max_blocks):
             check(d, max_blocks)
@@ -87,11 +90,13 @@ def test_large_and_small_windows():
     for _ in range(300):
         wbits = rnd.choice([0, 3, 8])
         wb = rnd.randrange(1 << wbits) if wbits else 0
-        k0 = rnd.choice([0, 1, 255, 70000, (1 << 24) - 1, 1 << 24, rnd.randrange(1 << 32), (1 << 32) + 5])
-        k1 = min(1 << 40, k0 + rnd.choice([1, 2, 7, 64, 5000, 1 << 20, 1 << 26, 1 << 31]))
+        k0 = rnd.choice([0, 1, 255, 70000, (1 << 24) - 1, 1 << 24, rnd.randrange(1 << 32), (1 << 32) + 5,
+                         rnd.randrange(1 << 40, 1 << 48), rnd.randrange(1 << 48, distpow.DPOW_K_LIMIT)])
+        k1 = min(distpow.DPOW_K_LIMIT, k0 + rnd.choice([1, 2, 7, 64, 5000, 1 << 20, 1 << 26, 1 << 31]))
         for max_blocks in (8, 1536):
-            for d in geometry([1, 2, 3, 4], wb, wbits, k0, k1, max_blocks):
-                check(d, max_blocks)
+            for nonce in ([1, 2, 3, 4], [1, 2]):  # SH 0; SH 2 (word W0+2 splits at L = 6)
+                for d in geometry(nonce, wb, wbits, k0, k1, max_blocks):
+                    check(d, max_blocks)
 
 
 def test_bench_step_is_one_launch():

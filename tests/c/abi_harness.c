@@ -6,9 +6,12 @@
  * (no GPU needed).  tests/test_abi.py builds and runs it.  On a host with a GPU
  * it also runs one search (argument "gpu").
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
 
 #include "dpow.h"
 #include "dpow_worker.h"
@@ -16,6 +19,26 @@
 static int fail(const char *what) {
     fprintf(stderr, "abi_harness: %s (%s)\n", what, dpow_last_error());
     return 1;
+}
+
+static void sleep_ms(long ms) {
+    struct timespec ts = {ms / 1000, (ms % 1000) * 1000000L};
+    nanosleep(&ts, NULL);
+}
+
+/* The Found/Cancel handler's side (worker.go:194,209): another thread raises the
+ * pinned flag while dpow_search runs. */
+static void *raise_cancel(void *ctx) {
+    sleep_ms(100);
+    *dpow_cancel_flag((dpow_ctx *)ctx) = 1u;
+    return NULL;
+}
+
+/* the worker's trace holds an action line naming `action` */
+static int traced(dpow_worker *w, const char *action) {
+    static char buf[1 << 16];
+    dpow_worker_trace(w, buf, sizeof buf);
+    return strstr(buf, action) != NULL;
 }
 
 int main(int argc, char **argv) {
@@ -38,16 +61,51 @@ int main(int argc, char **argv) {
     if (dpow_abi_version() != DPOW_ABI_VERSION) return fail("dpow_abi_version");
     if (dpow_search(NULL, nonce, 4, 6, 0, 0, 0, 1, NULL, secret, &len) != DPOW_EINVAL) return fail("NULL ctx");
     if (sizeof(dpow_worker_result) != 56 + DPOW_MAX_NONCE) return fail("dpow_worker_result layout");
+    const int gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
+    /* The worker mirror as worker.go's RPC shell would drive it (include/dpow_worker.h). */
+    dpow_worker *w = NULL;
+    dpow_worker_result res;
+    if (dpow_worker_new(0, &w) != 0) return fail("dpow_worker_new");
+    if (dpow_worker_mine(w, nonce, 4, 6, 0, 0, 11u) != 0) return fail("dpow_worker_mine");
+    if (dpow_worker_next_result(w, &res, 30000) != 0 || res.token != 11u) return fail("dpow_worker_next_result");
+    if (!gpu) {
+        /* no GPU: the failed search is reported at once, one message, the task is over */
+        if (res.error != DPOW_EHIP || res.has_secret || dpow_worker_active_tasks(w) != 0)
+            return fail("worker: failed search not reported");
+        if (!traced(w, "\"MinerError\"")) return fail("worker trace: MinerError");
+    } else {
+        /* config 2's answer, then the coordinator's Found kills the task: one nil ACK */
+        if (res.error != 0 || !res.has_secret || res.secret_len != 3 || res.secret[0] != 188 ||
+            res.secret[1] != 163 || res.secret[2] != 38)
+            return fail("worker: config 2 secret");
+        if (dpow_worker_found(w, nonce, 4, 6, 0, res.secret, res.secret_len, 11u) != 0)
+            return fail("dpow_worker_found");
+        if (dpow_worker_next_result(w, &res, 5000) != 0 || res.has_secret) return fail("worker: nil ACK");
+        if (dpow_worker_next_result(w, &res, 100) != DPOW_ETIMEOUT) return fail("worker: exactly two messages");
+        if (!traced(w, "\"WorkerResult\"") || !traced(w, "\"WorkerCancel\"")) return fail("worker trace");
+    }
+    dpow_worker_free(w);
     printf("{\"build_id\": \"%s\", \"abi\": %d, \"devices\": %d", dpow_build_id(), dpow_abi_version(),
            dpow_device_count());
-    if (argc > 1 && strcmp(argv[1], "gpu") == 0) {
+    if (gpu) {
         dpow_ctx *ctx = NULL;
         if (dpow_open(0, &ctx) != 0) return fail("dpow_open");
         uint64_t best = DPOW_NO_HIT;
-        const int rc = dpow_search(ctx, nonce, 4, 6, 0, 0, 0, 1u << 20, &best, secret, &len);
-        dpow_close(ctx);
+        int rc = dpow_search(ctx, nonce, 4, 6, 0, 0, 0, 1u << 20, &best, secret, &len);
         if (rc != DPOW_FOUND || best != 2532284u) return fail("dpow_search");
         printf(", \"search\": %llu", (unsigned long long)best);
+        /* an unreachable search (N = 32 over 2^40 k) stopped by the flag from another thread */
+        pthread_t th;
+        if (pthread_create(&th, NULL, raise_cancel, ctx) != 0) return fail("pthread_create");
+        best = DPOW_NO_HIT;
+        rc = dpow_search(ctx, nonce, 4, 32, 0, 0, 1u << 24, 1ull << 40, &best, secret, &len);
+        pthread_join(th, NULL);
+        *dpow_cancel_flag(ctx) = 0u;
+        if (rc != DPOW_CANCELLED) return fail("dpow_search: cancel flag from another thread");
+        rc = dpow_search(ctx, nonce, 4, 3, 0, 0, 0, 1u << 10, &best, secret, &len);  /* the ctx is reusable */
+        dpow_close(ctx);
+        if (rc != DPOW_FOUND || best != 97u) return fail("dpow_search after cancel");
+        printf(", \"cancelled\": true");
     }
     printf("}\n");
     return 0;

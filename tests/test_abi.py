@@ -85,13 +85,16 @@ def _build_c_harness(tmp_path):
     libdir = os.path.dirname(distpow.LIB_PATH)
     subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-pedantic",
                            "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c", "abi_harness.c"),
-                           "-L", libdir, "-ldpow", f"-Wl,-rpath,{libdir}", "-o", exe])
+                           "-L", libdir, "-ldpow", f"-Wl,-rpath,{libdir}", "-pthread", "-o", exe])
     return exe
 
 
 def test_c_abi_from_plain_c(tmp_path):
     """The headers are plain C11 (cgo compiles its preamble as C) and libdpow.so links and
-    runs from a C program: host entry points, argument checks, struct layout."""
+    runs from a C program: host entry points, argument checks, struct layout, and the
+    worker ABI (without a GPU its search fails and the error reaches the result channel).
+    On the GPU (test_c_abi_search_from_plain_c): a search, the worker's Mine -> result ->
+    Found -> nil ACK, and the cancel flag raised from another thread mid-search."""
     import json
     import distpow
     distpow.lib()  # the build-id check
@@ -104,4 +107,5 @@ def test_c_abi_from_plain_c(tmp_path):
 def test_c_abi_search_from_plain_c(tmp_path):
     import json
     out = subprocess.check_output([_build_c_harness(tmp_path), "gpu"], timeout=120).decode()
-    assert json.loads(out)["search"] == 2532284
+    rec = json.loads(out)
+    assert rec["search"] == 2532284 and rec["cancelled"] is True

@@ -54,6 +54,7 @@ def main():
         "sweep_launch_grid_threads": big,
         "sgpr_count": int(sweep[0]["SGPR_Count"]), "vgpr_count": int(sweep[0]["VGPR_Count"]),
         "candidates_per_sweep_launch": int(bench["roofline"]["candidates_per_launch"]),
+        "build_id": bench.get("build_id"),
     }
     pmc = {}
     for name in ("pmc_sq", "pmc_fetch", "pmc_write"):

@@ -39,7 +39,7 @@ CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 STRONG_TOTAL_PER_STEP = 1 << 38    # --strong: fixed total work per step
 K0 = 1 << 24                      # start of the L = 4 segment
 PROFILE_TAG = "r02"                # profiles/<tag>_summary.json of the current kernel
-TTS_BATCH_K = 1 << 8               # time-to-secret: first node batch (k), growing x4 up to 2^29 candidates per rank
+# time-to-secret at N > 1: node_mine's constant per-rank batch sized for N and the node (node.auto_batch_candidates)
 TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first_ms: the first, cold)
 # N > 1 time-to-secret: node_mine (batch-synchronous, RCCL all-reduce at batch boundaries,
 # the GPUs idle during it) unless DPOW_NODE_ASYNC=1 selects node_mine_async (ticked all-reduce
@@ -160,12 +160,11 @@ def main():
                 r = miner.mine(nonce, n)
                 res = NodeResult(r.status, r.global_idx, r.secret, 0, 0)
             elif NODE_SYNC:  # round 1's batch-synchronous node search
-                res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
-                                batch_k=TTS_BATCH_K, device=dev)
+                res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world, device=dev)
             else:  # no batch boundaries: ticked all-reduce + the node's best injected into each rank's search
                 res = node_mine_async(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
                                       bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
-                                      batch_k=TTS_BATCH_K, device=dev, tick_group=tick_group)
+                                      device=dev, tick_group=tick_group)
             barrier()
             runs.append((time.perf_counter() - t1) * 1e3)
             assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)

@@ -22,7 +22,7 @@ from typing import Callable, Optional, Sequence
 
 from ._lib import CANCELLED, DPOW_K_LIMIT, DPOW_NO_HIT, EXHAUSTED, FOUND
 
-__all__ = ["NodeResult", "node_mine", "node_mine_async", "partition_of_rank", "owner_rank"]
+__all__ = ["NodeResult", "auto_batch_candidates", "node_mine", "node_mine_async", "partition_of_rank", "owner_rank"]
 
 
 @dataclass
@@ -48,8 +48,33 @@ def owner_rank(global_idx: int, world: int) -> int:
     return (global_idx & 0xFF) >> (8 - b) if b else 0
 
 
+RANK_RATE = 2.17e11        # candidates/s of one MI355X on the one-block layouts (bench `value`)
+BATCH_OVERHEAD_S = 1e-4    # node_mine's fixed cost per batch: window launch + drain, all-reduce, host copies
+
+
+def auto_batch_candidates(num_trailing_zeros: int, world: int, rate: float = RANK_RATE,
+                          overhead_s: float = BATCH_OVERHEAD_S, lo: int = 1 << 16, hi: int = 1 << 31) -> int:
+    """Per-rank batch (candidates) that minimises the node's expected time to its first hit.
+
+    A candidate passes the suffix test (worker.go:246-256) with p = 16^-N: MD5's output
+    nibbles are uniform.  So the node's first hit is geometric and the search is
+    memoryless: every batch faces the same problem and the best batch is one constant
+    size.  With the node's hit rate lam = world * rate * p per second and a fixed cost c
+    per batch (every rank hashes its whole batch, then the all-reduce), the expected time
+    (c + t) / (1 - exp(-lam t)) ~ (1 / lam)(1 + c / t)(1 + lam t / 2) is smallest at
+    t = sqrt(2 c / lam): B = rate * t = sqrt(2 c rate / (world p)).  At 8 GPUs that is
+    0.15 M candidates per rank at N = 3, 2.4 M at N = 5, 9.5 M at N = 6, 38 M at N = 7,
+    152 M at N = 8 and 610 M at N = 9 (clamped to [2^16, 2^31]).  Growing from 2^8 k instead
+    (round 2's first schedule) spends 4-7 batch costs before a batch holds 0.1 ms of
+    hashing: more than the search itself at N <= 7.
+    """
+    p = 16.0 ** -min(max(num_trailing_zeros, 0), 32)
+    b = math.sqrt(2.0 * overhead_s * rate / (max(1, world) * p))
+    return int(min(hi, max(lo, b)))
+
+
 def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
-              batch_k: int = 1 << 8, k_start: int = 0, k_limit: int = DPOW_K_LIMIT, group=None,
+              batch_k: Optional[int] = None, k_start: int = 0, k_limit: int = DPOW_K_LIMIT, group=None,
               device=None, cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
               batch_k_max: Optional[int] = None, batch_candidates_max: int = 1 << 29) -> NodeResult:
     """Search until the first hit of the whole node (deterministic) or a cancel vote.
@@ -57,19 +82,22 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
     search_fn(nonce, ntz, worker_byte, worker_bits, k_begin, k_end, bound) -> SearchResult
     is this rank's one-window search (Miner.search for the GPU product).
 
-    Batches start at batch_k chunks and grow by `growth` up to batch_k_max (default:
-    batch_candidates_max = 2^29 candidates per rank, 2.5 ms of hashing; 2^24 k at 8
-    GPUs).  Every rank must finish a batch before the all-reduce, so a batch bounds the
-    overshoot past the hit: small first batches keep small N at a few short batches.
-    The cap trades the per-batch cost c (the window's launch and drain, the all-reduce
-    and the host round trip, ~0.1 ms) against the overshoot (about half the last batch):
-    for T ms of hashing per rank the sum c T / B + B / 2 is smallest near B = sqrt(2 c T),
-    2.3 ms for N = 9 at 8 GPUs (~26 ms per rank).  (Round 1 capped at 2^22 k, 0.6 ms.)
+    Every rank must finish a batch before the all-reduce, so a batch bounds the
+    overshoot past the hit, and each batch costs a fixed c on top of its hashing.
+    - batch_k None (default): one constant batch per rank sized for N and the node
+      (auto_batch_candidates, the expected-time optimum of the geometric first hit).
+    - batch_k given: batches start at batch_k chunks and grow by `growth` up to
+      batch_k_max (default: batch_candidates_max = 2^29 candidates per rank, 2.5 ms of
+      hashing; 2^24 k at 8 GPUs).  For T ms of hashing per rank, c T / B + B / 2 is
+      smallest near B = sqrt(2 c T), 2.3 ms for N = 9 at 8 GPUs.
     """
     import torch
     import torch.distributed as dist
 
     wb, wbits = partition_of_rank(rank, world)
+    if batch_k is None:
+        batch_k = max(1, auto_batch_candidates(num_trailing_zeros, world) >> (8 - wbits % 9))
+        growth = 1
     if batch_k_max is None:
         batch_k_max = max(1, batch_candidates_max >> (8 - wbits % 9))
     dist_on = world > 1 and dist.is_available() and dist.is_initialized()

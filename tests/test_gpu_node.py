@@ -44,7 +44,10 @@ def _rank_main(rank, world, port, cases, out_q):
     with distpow.Miner(0) as m:
         search = lambda *a: m.search(*a[:6], bound=a[6])  # noqa: E731  (node_mine's search_fn)
         for nonce, ntz in cases:
+            # the growing schedule (2^8 k, x4) and the default constant batch (auto_batch_candidates)
             r = node_mine(search, nonce, ntz, rank, world, batch_k=1 << 8)
+            res.append((r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner, r.batches))
+            r = node_mine(search, nonce, ntz, rank, world)
             res.append((r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner, r.batches))
         # the asynchronous node search: no batch boundaries, the node's best hit injected
         # into every rank's running search (Miner.bound -> dpow_search_bound)
@@ -88,13 +91,14 @@ def test_node_mine_two_ranks_on_gpu(golden):
             if p.is_alive():
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
-    n = len(cases)
+    n = 2 * len(cases)
     for rank in range(world):
-        for (nonce, ntz), (status, g, secret, owner, batches) in zip(cases, outs[rank][:n]):
+        for (nonce, ntz), (status, g, secret, owner, batches) in zip([c for c in cases for _ in (0, 1)],
+                                                                     outs[rank][:n]):
             e = exp[(tuple(nonce), ntz)]
             assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, nonce, ntz, g)
             assert owner == (g & 0xFF) >> 7
-        for (nonce, ntz), (tag, status, g, secret, owner) in zip(cases, outs[rank][n:2 * n]):
+        for (nonce, ntz), (tag, status, g, secret, owner) in zip(cases, outs[rank][n:n + len(cases)]):
             e = exp[(tuple(nonce), ntz)]
             assert tag == "async" and status == 1 and g == e["global_idx"] and secret == e["secret"], \
                 (rank, nonce, ntz, g)

@@ -131,3 +131,20 @@ def test_node_mine_gloo_matches_wbits0_answer(golden, world):
         assert res[-1] == (2, 1)  # CANCELLED after the first batch on every rank
     # all ranks agree batch by batch
     assert len({tuple(map(tuple, [r[:2] for r in outs[k][:-1]])) for k in outs}) == 1
+
+
+def test_auto_batch_schedule():
+    """node_mine's default batch: sqrt(2 c rate / (world p)) with p = 16^-N, clamped."""
+    import math
+    from distpow.node import BATCH_OVERHEAD_S, RANK_RATE, auto_batch_candidates
+    lo, hi = 1 << 16, 1 << 31
+    for world in (1, 2, 4, 8):
+        seq = [auto_batch_candidates(n, world) for n in range(0, 34)]
+        assert all(lo <= b <= hi for b in seq)
+        assert seq == sorted(seq)  # rarer hits -> longer batches
+        assert seq[0] == lo and seq[-1] == hi
+        for n in (5, 6, 7, 8, 9):  # unclamped: the expected-time optimum
+            want = math.sqrt(2 * BATCH_OVERHEAD_S * RANK_RATE / (world * 16.0 ** -n))
+            assert abs(auto_batch_candidates(n, world) - want) <= 1
+    # more GPUs -> a shorter batch per rank (the node's hit rate grows), ratio sqrt(world)
+    assert auto_batch_candidates(8, 1) / auto_batch_candidates(8, 8) == pytest.approx(math.sqrt(8), rel=1e-6)

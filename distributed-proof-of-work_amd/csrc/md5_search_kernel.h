@@ -71,6 +71,14 @@ namespace dpow {
 #ifndef DPOW_HEAD_PRIO
 #define DPOW_HEAD_PRIO 0  // A/B switch (needs DPOW_TAIL_PRIO)
 #endif
+// A wave requests its next claim while it hashes the current chunk (1), or only
+// once that chunk is done (0: one claim in flight per wave, so a first hit
+// waits for fewer chunks below it; A/B switch).  profiles/r02_ab_ahead.log:
+// 1 / 0 -> 217.6 / 215.5 GH/s, time-to-secret N = 7 1.35-1.40 / 1.33-1.34 ms, N = 8
+// 19.1 / 19.3 ms: the claim's latency shows, the shorter drain does not.
+#ifndef DPOW_CLAIM_AHEAD
+#define DPOW_CLAIM_AHEAD 1
+#endif
 constexpr uint32_t kPollWb = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 1;
 // Diagnostic builds only (tools/wave_trace.py): every worker wave records
 // {start, first claim, exit} in s_memrealtime ticks (100 MHz) and its hashed
@@ -787,7 +795,9 @@ DPOW_DEV void search_body(const Launch &L) {
 #else
         if (claim >= L.n_chunks) break;
 #endif
+#if DPOW_CLAIM_AHEAD
         const uint64_t next = claim_next(L.claim + x * kClaimStride, x, lane);
+#endif
         // Claims [0, n_big) are `chunk` wave-blocks, the rest `chunk_tail`: the
         // launch ends on small claims, so its waves run dry within a few
         // wave-blocks of each other (the tail of a 2.5 ms launch was ~3 %).
@@ -877,7 +887,12 @@ DPOW_DEV void search_body(const Launch &L) {
         best = best_next < best ? best_next : best;
         stop = stop_next;
 #endif
+#if DPOW_CLAIM_AHEAD
         claim = next;
+#else
+        if (stop != 0u) break;
+        claim = claim_next(L.claim + x * kClaimStride, x, lane);
+#endif
     }
     // Retirement is counted per workgroup (a quarter of the atomics on the
     // shared counter).  Each wave's atomicMin has been performed already (the

@@ -79,6 +79,9 @@ namespace dpow {
 #ifndef DPOW_CLAIM_AHEAD
 #define DPOW_CLAIM_AHEAD 1
 #endif
+#ifndef DPOW_CLAIM_DEFER
+#define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch)
+#endif
 constexpr uint32_t kPollWb = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 1;
 // Diagnostic builds only (tools/wave_trace.py): every worker wave records
 // {start, first claim, exit} in s_memrealtime ticks (100 MHz) and its hashed
@@ -629,14 +632,23 @@ DPOW_DEV void watcher(const Launch &L) {
     }
 }
 
-// One returning atomic per claim, by lane 0, broadcast to the wave; the
-// counter's n-th claim is chunk n * kClaimCounters + x.
-DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t x, uint32_t lane) {
+// One returning atomic per claim, by lane 0 (claim_issue); its result stays in
+// lane 0's VGPR until claim_take broadcasts it to the wave -- the wave waits for
+// the atomic only there.  The counter's n-th claim is chunk n * kClaimCounters + x.
+DPOW_DEV unsigned long long claim_issue(unsigned long long *ctr, uint32_t lane) {
     unsigned long long v = 0;
     if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+
+DPOW_DEV uint64_t claim_take(unsigned long long v, uint32_t x) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
     return (((uint64_t)hi << 32) | lo) * kClaimCounters + x;
+}
+
+DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t x, uint32_t lane) {
+    return claim_take(claim_issue(ctr, lane), x);
 }
 
 DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
@@ -795,7 +807,11 @@ DPOW_DEV void search_body(const Launch &L) {
 #else
         if (claim >= L.n_chunks) break;
 #endif
-#if DPOW_CLAIM_AHEAD
+#if DPOW_CLAIM_AHEAD && DPOW_CLAIM_DEFER
+        // The next claim's atomic is issued now and its result read after this chunk
+        // (claim_take): the wave hashes while the atomic is in flight.
+        const unsigned long long next_v = claim_issue(L.claim + x * kClaimStride, lane);
+#elif DPOW_CLAIM_AHEAD
         const uint64_t next = claim_next(L.claim + x * kClaimStride, x, lane);
 #endif
         // Claims [0, n_big) are `chunk` wave-blocks, the rest `chunk_tail`: the
@@ -887,7 +903,9 @@ DPOW_DEV void search_body(const Launch &L) {
         best = best_next < best ? best_next : best;
         stop = stop_next;
 #endif
-#if DPOW_CLAIM_AHEAD
+#if DPOW_CLAIM_AHEAD && DPOW_CLAIM_DEFER
+        claim = claim_take(next_v, x);
+#elif DPOW_CLAIM_AHEAD
         claim = next;
 #else
         if (stop != 0u) break;

@@ -175,7 +175,7 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks_
     }
     // Guided tail: the last ~kTailClaimsPerWave claims per wave are kMinChunk
     // wave-blocks, so the waves of a launch run dry together.
-    const uint64_t chunk_tail = kMinChunk < chunk ? kMinChunk : chunk;
+    const uint64_t chunk_tail = kTailChunk < chunk ? kTailChunk : chunk;
     const uint64_t tail_wb = worker_blocks * wpb * kTailClaimsPerWave * chunk_tail;
     const uint64_t n_big = L.n_wblocks > tail_wb ? (L.n_wblocks - tail_wb) / chunk : 0;
     const uint64_t rest = L.n_wblocks - n_big * chunk;
@@ -186,6 +186,10 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks_
     if (need_blocks < n_chunks && need_blocks < kClaimCounters)
         need_blocks = n_chunks < kClaimCounters ? n_chunks : kClaimCounters;
     if (worker_blocks > need_blocks) worker_blocks = need_blocks;
+    // Tail claims smaller than a workgroup's share (kTailChunk < kMinChunk) can give a
+    // few-wave-block launch more claims than its wave-block count asked workgroups for.
+    const uint64_t min_blocks = n_chunks < kClaimCounters ? n_chunks : kClaimCounters;
+    if (worker_blocks < min_blocks && min_blocks <= max_blocks) worker_blocks = min_blocks;
     if (worker_blocks < kClaimCounters && worker_blocks < n_chunks) return DPOW_EINVAL;
     L.chunk = (uint32_t)chunk;
     L.chunk_tail = (uint32_t)chunk_tail;

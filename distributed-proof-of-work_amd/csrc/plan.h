@@ -62,7 +62,12 @@ constexpr uint64_t kMaxChunk = DPOW_MAX_CHUNK;  // ... and at most
 #define DPOW_TAIL_CLAIMS 2  // small claims per wave at the end of a launch (0: none; A/B switch)
 #endif
 constexpr uint64_t kTailClaimsPerWave = DPOW_TAIL_CLAIMS;
-static_assert((kMinChunk & (kMinChunk - 1)) == 0 && (kMaxChunk & (kMaxChunk - 1)) == 0,
+#ifndef DPOW_TAIL_CHUNK
+#define DPOW_TAIL_CHUNK 4  // wave-blocks per tail claim (at most the launch's chunk; A/B switch)
+#endif
+constexpr uint64_t kTailChunk = DPOW_TAIL_CHUNK;
+static_assert((kMinChunk & (kMinChunk - 1)) == 0 && (kMaxChunk & (kMaxChunk - 1)) == 0 &&
+                  (kTailChunk & (kTailChunk - 1)) == 0 && kTailChunk <= kMinChunk,
               "chunk bounds are powers of two (segment alignment)");
 int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks);
 

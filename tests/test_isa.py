@@ -58,3 +58,29 @@ def test_pipeline_order_and_padding(kernel_110):
     # no half-rate instruction is directly followed by another VALU inside the pipeline
     body = seq[seq.find(group):seq.rfind(group) + len(group)]
     assert "HF" not in body and "HH" not in body
+
+
+def test_claim_ahead_latency_hidden(kernel_110):
+    """The claim requested ahead of a chunk (md5_search_kernel.h, DPOW_CLAIM_DEFER) is read
+    after the chunk: its atomic precedes the hash block and the readfirstlane of its
+    result follows it, so the wave hashes while the atomic is in flight.  (The AMDGPU
+    atomic optimizer, off for these TUs via csrc/Makefile VFLAGS, would read it at once.)"""
+    isa_loop, lines = kernel_110
+    hash_lo = min(b[0] for b in isa_loop.hash_block_mix(lines))
+    ins = []
+    for l in lines:
+        m = re.search(r"//\s*([0-9A-F]{6,}):", l)
+        if m:
+            ins.append((int(m.group(1), 16), l.split("//")[0].strip()))
+    base = ins[0][0]
+    hidden = False
+    for i, (a, text) in enumerate(ins):
+        m = re.match(r"global_atomic_add_x2 v\[(\d+):(\d+)\]", text)
+        if not m or a - base >= hash_lo:
+            continue
+        regs = {f"v{m.group(1)}", f"v{m.group(2)}"}
+        for a2, t2 in ins[i + 1:]:
+            if t2.startswith("v_readfirstlane_b32") and t2.split(",")[-1].strip() in regs:
+                hidden |= a2 - base > hash_lo
+                break
+    assert hidden, "every claim atomic is waited for before the hash block"

@@ -13,6 +13,7 @@
 // the next search on the context.
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <sys/prctl.h>
 #include <time.h>
 
 #include <atomic>
@@ -35,6 +36,7 @@ using namespace dpow;
 namespace {
 
 thread_local std::string g_last_error;
+thread_local bool g_slack_set = false;  // this thread's timer slack lowered (wait_record)
 
 int set_error(int code, const std::string &msg) {
     g_last_error = msg;
@@ -67,10 +69,8 @@ constexpr int DPOW_BOUNDED = 3;
 // youngest ones hash ~1/60 of the mean and sit on the early chunks they
 // claimed, which a first hit has to wait for.  6 vs 8 (profiles/r01_ab_tail_prio.log):
 // throughput equal in every layout, time-to-secret N = 7 1.49 -> 1.37 ms.
-#ifndef DPOW_BLOCKS_PER_CU
-#define DPOW_BLOCKS_PER_CU 6
-#endif
-constexpr uint64_t kBlocksPerCu = DPOW_BLOCKS_PER_CU;
+// (The grid of a short launch is smaller: plan.h launch_blocks_per_cu.)
+constexpr uint64_t kBlocksPerCu = kMaxBlocksPerCu;
 // Claim-counter slots (kClaimSlot counters each) used round-robin by the launches
 // of a search: zeroed at search start, re-zeroed by each launch's last workgroup.
 constexpr size_t kClaimRing = 64;
@@ -181,6 +181,12 @@ int wait_record(dpow_ctx *c, uint64_t seq) {
         if (spinning) {
             __builtin_ia32_pause();
         } else {
+            // Linux pads a normal thread's nanosleep by its 50 us default timer slack,
+            // which a hit's record would wait out; 1 us keeps the poll at ~kPollNs.
+            if (!g_slack_set) {
+                (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+                g_slack_set = true;
+            }
             const struct timespec ts = {0, kPollNs};
             nanosleep(&ts, nullptr);
         }
@@ -390,6 +396,10 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
     return (int)n;
 }
 
+uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t worker_bits) {
+    return launch_blocks_per_cu(candidates, ntz, remainder_bits(worker_bits));
+}
+
 int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint64_t k, uint32_t iv_d,
                          uint32_t state_d) {
     std::vector<PlannedLaunch> plan;
@@ -496,7 +506,8 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
         Launch &L = pl.L;
         // This search's share of the device's resident workgroups (1 / searches in flight on it).
         const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
-        const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * kBlocksPerCu / share, kClaimCounters);
+        const uint64_t bpc = launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
+        const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * bpc / share, kClaimCounters);
         uint64_t worker_blocks = 0;
         rc = size_launch(pl, max_blocks, &worker_blocks);
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");

@@ -200,4 +200,18 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks_
     return 0;
 }
 
+uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits) {
+#if DPOW_SMALL_GRIDS
+    // Candidates of this partition expected before its first hit: 16^N R / 256.
+    uint64_t expect = ~0ull;
+    if (ntz < 14) expect = ((1ull << (4 * ntz)) << rbits) >> 8;
+    const uint64_t eff = candidates < expect ? candidates : expect;
+    if (eff <= (1ull << 22)) return 3;
+    if (eff <= (1ull << 24)) return 4;
+#else
+    (void)candidates, (void)ntz, (void)rbits;
+#endif
+    return kMaxBlocksPerCu;
+}
+
 }  // namespace dpow

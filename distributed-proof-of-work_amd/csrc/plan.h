@@ -71,4 +71,20 @@ static_assert((kMinChunk & (kMinChunk - 1)) == 0 && (kMaxChunk & (kMaxChunk - 1)
               "chunk bounds are powers of two (segment alignment)");
 int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks);
 
+// Worker workgroups per CU for one launch (before the device share).  The full
+// persistent grid (kMaxBlocksPerCu = 6) has the highest rate, but a launch that is
+// short -- few candidates, or a first hit expected early (16^N candidates of the
+// whole enumeration, 16^N R / 256 of this partition) -- finishes sooner with fewer
+// waves: 3 per CU up to 2^22 expected candidates, 4 up to 2^24
+// (profiles/r02_ab_blocks.log, r02_ab_grid/: time-to-secret N = 6 0.22 -> 0.15 ms, N = 5 0.104 ->
+// 0.086 ms; windows of 2^22 / 2^24 candidates 50 -> 43 / 120 -> 110 us).
+#ifndef DPOW_BLOCKS_PER_CU
+#define DPOW_BLOCKS_PER_CU 6
+#endif
+#ifndef DPOW_SMALL_GRIDS
+#define DPOW_SMALL_GRIDS 1  // fewer workgroups per CU for short launches (A/B switch)
+#endif
+constexpr uint64_t kMaxBlocksPerCu = DPOW_BLOCKS_PER_CU;
+uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits);
+
 }  // namespace dpow

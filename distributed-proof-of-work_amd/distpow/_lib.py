@@ -177,6 +177,7 @@ def lib():
                                                ctypes.POINTER(ctypes.c_double)]),
         "dpow_diag_dword_test": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64,
                                                 ctypes.c_uint32, ctypes.c_uint32]),
+        "dpow_diag_blocks_per_cu": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
         "dpow_worker_new": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
         "dpow_worker_free": (None, [vp]),
         "dpow_worker_mine": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
@@ -190,6 +191,8 @@ def lib():
         "dpow_worker_active_tasks": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
+        if LIB_OVERRIDE and name.startswith("dpow_diag_") and not hasattr(L, name):
+            continue  # an older A/B build (tools/ab_variants.py) may lack a newer diagnostic
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

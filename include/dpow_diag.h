@@ -70,6 +70,12 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
                               uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,
                               uint64_t max_blocks, dpow_diag_launch *out, size_t max_launches);
 
+/* Worker workgroups per CU dpow_search gives a launch of `candidates` local indices
+ * at (ntz, worker_bits), before dividing by the searches sharing the device: 6 (the
+ * full persistent grid) unless the launch is short -- at most 2^24 candidates, or a
+ * first hit expected within that many (16^ntz R / 256) -- then 4, or 3 at 2^22. */
+uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t worker_bits);
+
 #ifdef __cplusplus
 }
 #endif

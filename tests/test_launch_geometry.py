@@ -106,3 +106,19 @@ def test_bench_step_is_one_launch():
         ds = geometry([1, 2, 3, 4], wb, wbits, 1 << 24, (1 << 24) + nk, 1536)
         assert len(ds) == 1 and ds[0].chunk == 32 and ds[0].worker_blocks == 1536
         check(ds[0], 1536)
+
+
+def test_grid_policy_for_short_launches():
+    """dpow_search's workgroups per CU (plan.cpp launch_blocks_per_cu): the full persistent
+    grid for long launches with no early hit expected (the sweep), smaller grids for short
+    launches or an expected early hit (16^N R / 256 candidates of this partition)."""
+    from distpow._lib import lib
+    f = lib().dpow_diag_blocks_per_cu
+    assert f(1 << 36, 32, 0) == 6 and f(1 << 36, 32, 3) == 6       # the bench sweep, 1 and 8 GPUs
+    assert f(1 << 22, 32, 0) == 3 and f(1 << 24, 32, 0) == 4 and f((1 << 24) + 1, 32, 0) == 6
+    assert f(1 << 32, 6, 0) == 4 and f(1 << 32, 5, 0) == 3 and f(1 << 32, 7, 0) == 6  # 16^N expected
+    assert f(1 << 32, 6, 3) == 3        # 16^6 * 32 / 256 = 2^21 candidates of a workerBits-3 partition
+    assert f(1 << 32, 0, 0) == 3 and f(0, 32, 0) == 3
+    for n in range(0, 40, 3):  # never more than the full grid, monotone in the launch size
+        seq = [f(1 << n, z, 0) for z in range(0, 34)]
+        assert all(3 <= b <= 6 for b in seq) and seq == sorted(seq)

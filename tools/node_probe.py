@@ -65,6 +65,32 @@ def main():
                 out["tts_ms"][f"G{G} {bytes(nonce).hex()}/{n}"] = row
                 print(f"G{G} {bytes(nonce).hex()}/{n}: grow {row['grow']['ms']} ms ({row['grow']['batches']} b), "
                       f"auto {row['auto']['ms']} ms ({row['auto']['batches']} b)", file=sys.stderr, flush=True)
+        # Every rank of the node (sync schedule): a rank hashes its batches up to and
+        # including the one that holds the answer, or stops at its own first hit in it;
+        # the node's time is the slowest rank's (plus one all-reduce per batch).
+        out["node_ms"] = {}
+        for G in (2, 8):
+            for nonce, n in want:
+                g = exp[(tuple(nonce), n)]
+                rb = 8 - (G.bit_length() - 1)
+                bk = max(1, auto_batch_candidates(n, G) >> rb)
+                k_lim = ((g >> 8) // bk + 1) * bk
+                per_rank = []
+                for r in range(G):
+                    ts = []
+                    for _ in range(runs):
+                        torch.cuda.synchronize()
+                        t = time.perf_counter()
+                        res = node_mine(search, nonce, n, r, G, device=dev, k_limit=k_lim)
+                        ts.append((time.perf_counter() - t) * 1e3)
+                        assert res.status in (distpow.FOUND, distpow.EXHAUSTED)
+                        assert res.status != distpow.FOUND or res.global_idx >= g
+                    per_rank.append(round(sorted(ts)[len(ts) // 2], 3))
+                key = f"G{G} {bytes(nonce).hex()}/{n}"
+                out["node_ms"][key] = {"max_rank_ms": max(per_rank), "owner_ms": per_rank[owner_rank(g, G)],
+                                       "per_rank_ms": per_rank}
+                print(f"node {key}: slowest rank {max(per_rank)} ms, owner {per_rank[owner_rank(g, G)]} ms",
+                      file=sys.stderr, flush=True)
     out["build_id"] = distpow.build_id()
     print(json.dumps(out, indent=1))
 

@@ -80,7 +80,8 @@ namespace dpow {
 #define DPOW_CLAIM_AHEAD 1
 #endif
 #ifndef DPOW_CLAIM_DEFER
-#define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch)
+#define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch;
+                            // one final block only, search_body kDeferClaims)
 #endif
 constexpr uint32_t kPollWb = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 1;
 // Diagnostic builds only (tools/wave_trace.py): every worker wave records
@@ -635,8 +636,19 @@ DPOW_DEV void watcher(const Launch &L) {
 // One returning atomic per claim, by lane 0 (claim_issue); its result stays in
 // lane 0's VGPR until claim_take broadcasts it to the wave -- the wave waits for
 // the atomic only there.  The counter's n-th claim is chunk n * kClaimCounters + x.
+// The AMDGPU atomic optimizer rewrites an atomic on a uniform address into a wave-wide
+// reduction that reads the returned value at once, which would put the atomic's latency
+// back in front of the chunk it was issued ahead of.  A lane-varying (opaque) zero offset
+// keeps the address divergent to the compiler, so the claim stays a plain one-lane
+// returning atomic, waited for only where claim_take reads it.
+template <bool kOpaque>
 DPOW_DEV unsigned long long claim_issue(unsigned long long *ctr, uint32_t lane) {
     unsigned long long v = 0;
+    if constexpr (kOpaque) {
+        uint32_t z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        ctr += z;
+    }
     if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v;
 }
@@ -648,7 +660,7 @@ DPOW_DEV uint64_t claim_take(unsigned long long v, uint32_t x) {
 }
 
 DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t x, uint32_t lane) {
-    return claim_take(claim_issue(ctr, lane), x);
+    return claim_take(claim_issue<false>(ctr, lane), x);
 }
 
 DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
@@ -783,6 +795,11 @@ DPOW_DEV void search_body(const Launch &L) {
     __builtin_amdgcn_s_setprio(1);
 #endif
 #endif
+    // The deferred claim read holds the claim's value in two more VGPRs across the hash
+    // loop; the two-block kernels sit at 71-79 VGPRs, where that costs a wave per SIMD
+    // or shifts their register assignment (-5 to -10 %, profiles/r02_ab_layouts/), so
+    // they keep the claim read in front of the chunk.
+    constexpr bool kDeferClaims = DPOW_CLAIM_DEFER && NBLK == 1;
     uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
     uint64_t claim = skip ? L.n_chunks : claim_next(L.claim + x * kClaimStride, x, lane);
@@ -807,12 +824,13 @@ DPOW_DEV void search_body(const Launch &L) {
 #else
         if (claim >= L.n_chunks) break;
 #endif
-#if DPOW_CLAIM_AHEAD && DPOW_CLAIM_DEFER
-        // The next claim's atomic is issued now and its result read after this chunk
-        // (claim_take): the wave hashes while the atomic is in flight.
-        const unsigned long long next_v = claim_issue(L.claim + x * kClaimStride, lane);
-#elif DPOW_CLAIM_AHEAD
-        const uint64_t next = claim_next(L.claim + x * kClaimStride, x, lane);
+#if DPOW_CLAIM_AHEAD
+        // With kDeferClaims the next claim's atomic is issued now and its result read after
+        // this chunk (claim_take): the wave hashes while the atomic is in flight.
+        unsigned long long next_v = 0;
+        uint64_t next = 0;
+        if constexpr (kDeferClaims) next_v = claim_issue<true>(L.claim + x * kClaimStride, lane);
+        else next = claim_next(L.claim + x * kClaimStride, x, lane);
 #endif
         // Claims [0, n_big) are `chunk` wave-blocks, the rest `chunk_tail`: the
         // launch ends on small claims, so its waves run dry within a few
@@ -903,10 +921,9 @@ DPOW_DEV void search_body(const Launch &L) {
         best = best_next < best ? best_next : best;
         stop = stop_next;
 #endif
-#if DPOW_CLAIM_AHEAD && DPOW_CLAIM_DEFER
-        claim = claim_take(next_v, x);
-#elif DPOW_CLAIM_AHEAD
-        claim = next;
+#if DPOW_CLAIM_AHEAD
+        if constexpr (kDeferClaims) claim = claim_take(next_v, x);
+        else claim = next;
 #else
         if (stop != 0u) break;
         claim = claim_next(L.claim + x * kClaimStride, x, lane);

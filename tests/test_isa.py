@@ -63,8 +63,9 @@ def test_pipeline_order_and_padding(kernel_110):
 def test_claim_ahead_latency_hidden(kernel_110):
     """The claim requested ahead of a chunk (md5_search_kernel.h, DPOW_CLAIM_DEFER) is read
     after the chunk: its atomic precedes the hash block and the readfirstlane of its
-    result follows it, so the wave hashes while the atomic is in flight.  (The AMDGPU
-    atomic optimizer, off for these TUs via csrc/Makefile VFLAGS, would read it at once.)"""
+    result follows it, so the wave hashes while the atomic is in flight.  (On a uniform
+    address the AMDGPU atomic optimizer would rewrite the atomic into a wave reduction that
+    reads it at once; claim_issue keeps the address opaque.)"""
     isa_loop, lines = kernel_110
     hash_lo = min(b[0] for b in isa_loop.hash_block_mix(lines))
     ins = []

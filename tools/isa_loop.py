@@ -26,8 +26,7 @@ def disasm(csrc, nblk, sh, extra):
     tmp = tempfile.mkdtemp()
     o, co = os.path.join(tmp, "v.o"), os.path.join(tmp, "v.co")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-DDPOW_NC=2", "--offload-arch=gfx950",
-                           "-munsafe-fp-atomics", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",  # = csrc/Makefile VFLAGS
-                           f"-DDPOW_VNBLK={nblk}", f"-DDPOW_VSH={sh}", *extra,
+                           "-munsafe-fp-atomics", f"-DDPOW_VNBLK={nblk}", f"-DDPOW_VSH={sh}", *extra,
                            "--cuda-device-only", "-c", "md5_variant.hip", "-o", o], cwd=csrc)
     subprocess.check_call([f"{LLVM}/clang-offload-bundler", "--type=o", f"--input={o}", "--unbundle",
                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"])

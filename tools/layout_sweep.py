@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Sweep throughput per message layout (nonce length -> kernel variant <NBLK, W0, SH>).
 
-    python tools/layout_sweep.py [log2_candidates] [rounds]
+    python tools/layout_sweep.py [log2_candidates] [rounds] [nonce lengths, comma-separated]
 
 For each nonce length, hashes 2^n candidates (default 2^34) of an all-0x5a nonce at
 N = 32 (unreachable) in the L = 4 chunk segment and prints the kernel GH/s (HIP-event
@@ -22,6 +22,8 @@ NK = (1 << LOG2) >> 8
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 LENGTHS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 24, 32, 40, 48, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60,
            61, 62, 63, 64, 68, 100, 120)
+if len(sys.argv) > 3:
+    LENGTHS = tuple(int(x) for x in sys.argv[3].split(","))
 out = {}
 with distpow.Miner(0) as m:
     m.search([1, 2, 3, 4], 32, 0, 0, K0, K0 + NK)  # warm the clocks on a full-size run first

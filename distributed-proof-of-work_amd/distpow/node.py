@@ -105,6 +105,10 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
         backend = dist.get_backend(group) if dist_on else "gloo"
         device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     buf = torch.empty(2, dtype=torch.int64, device=device)
+    # With a device buffer (RCCL), a pinned host twin carries the values in and out:
+    # stream-ordered copies around the all-reduce and one stream synchronize per batch.
+    on_gpu = buf.device.type == "cuda"
+    hbuf = torch.empty(2, dtype=torch.int64, pin_memory=True) if on_gpu else buf
     bound = DPOW_NO_HIT
     secret = None
     k = k_start
@@ -117,13 +121,16 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
         if r.status == FOUND:
             secret = r.secret
         running = 0 if (r.status == CANCELLED or cancelled()) else 1
-        # one host->device copy in and one device->host copy out per batch (each is a
-        # synchronous round trip of tens of microseconds with RCCL's device tensors)
-        buf.copy_(torch.tensor([mine, running], dtype=torch.int64))
+        hbuf[0], hbuf[1] = mine, running
+        if on_gpu:
+            buf.copy_(hbuf, non_blocking=True)
         if dist_on:
             dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
+        if on_gpu:
+            hbuf.copy_(buf, non_blocking=True)
+            torch.cuda.current_stream(buf.device).synchronize()
         batches += 1
-        best, all_running = (int(x) for x in buf.tolist())
+        best, all_running = (int(x) for x in hbuf.tolist())
         if best != DPOW_NO_HIT:
             own = owner_rank(best, world)
             if best != mine:

@@ -145,8 +145,8 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
 
 def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
                     bound_fn: Callable[[int], None] = lambda g: None, cancel_fn: Callable[[], None] = lambda: None,
-                    clear_fn: Callable[[], None] = lambda: None, batch_k: int = 1 << 8, k_start: int = 0,
-                    k_limit: int = DPOW_K_LIMIT, group=None, device=None,
+                    clear_fn: Callable[[], None] = lambda: None, batch_k: Optional[int] = None,
+                    k_start: int = 0, k_limit: int = DPOW_K_LIMIT, group=None, device=None,
                     cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
                     batch_candidates_max: int = 1 << 31, tick_s: float = 1e-4,
                     sync_candidates: int = 1 << 27, tick_group=None, tick_device=None) -> NodeResult:
@@ -168,7 +168,8 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
     the pinned cancel flag to end the in-flight search at the end.
 
     The first sync_candidates per rank (2^27: 0.6 ms of hashing) run as node_mine's
-    synchronous batches: a small N ends there without a thread or a tick (the ticked
+    synchronous batches (batch_k None: its constant expected-time batch; else growing from
+    batch_k): a small N ends there without a thread or a tick (the ticked
     loop costs a few hundred microseconds of latency, which only pays on longer searches).
 
     tick_group / tick_device: where the ticks' all-reduce runs (default: group / device).
@@ -189,8 +190,10 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
         if r.status != EXHAUSTED or k_switch >= k_limit:
             return r
         # continue with windows about the size of the synchronous phase's last batches
-        batch_k = max(batch_k, (k_switch - k_start) >> 1)
+        batch_k = max(batch_k or 1, (k_switch - k_start) >> 1)
         k_start = k_switch
+    if batch_k is None:
+        batch_k = max(1, auto_batch_candidates(num_trailing_zeros, world) >> rbits)
     batch_k_max = max(1, batch_candidates_max >> rbits)
     dist_on = world > 1 and dist.is_available() and dist.is_initialized()
     if device is None:

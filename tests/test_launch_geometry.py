@@ -93,7 +93,7 @@ def test_large_and_small_windows():
         k0 = rnd.choice([0, 1, 255, 70000, (1 << 24) - 1, 1 << 24, rnd.randrange(1 << 32), (1 << 32) + 5,
                          rnd.randrange(1 << 40, 1 << 48), rnd.randrange(1 << 48, distpow.DPOW_K_LIMIT)])
         k1 = min(distpow.DPOW_K_LIMIT, k0 + rnd.choice([1, 2, 7, 64, 5000, 1 << 20, 1 << 26, 1 << 31]))
-        for max_blocks in (8, 1536):
+        for max_blocks in (8, 96, 768, 1024, 1536):  # shares and the 3 / 4 / 6-per-CU grids
             for nonce in ([1, 2, 3, 4], [1, 2]):  # SH 0; SH 2 (word W0+2 splits at L = 6)
                 for d in geometry(nonce, wb, wbits, k0, k1, max_blocks):
                     check(d, max_blocks)

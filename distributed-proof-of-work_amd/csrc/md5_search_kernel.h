@@ -945,6 +945,14 @@ DPOW_DEV void search_body(const Launch &L) {
         g_wave_trace[4 * wave + 3] = n_wb;
     }
 #endif
+    if constexpr (kDeferClaims) {
+        // A wave that left the loop right after issuing its next claim (a hit below the
+        // chunk, a bound, a cancel) still has that atomic in flight; the last retiring
+        // workgroup re-zeroes the launch's claim counters in publish(), and a claim
+        // landing after that would leave the slot's next user one chunk short.  Every
+        // claim of the workgroup is performed before its retirement count.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -206,8 +206,8 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits)
     uint64_t expect = ~0ull;
     if (ntz < 14) expect = ((1ull << (4 * ntz)) << rbits) >> 8;
     const uint64_t eff = candidates < expect ? candidates : expect;
-    if (eff <= (1ull << 22)) return 3;
-    if (eff <= (1ull << 24)) return 4;
+    if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
+    if (eff <= (1ull << 24)) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
 #else
     (void)candidates, (void)ntz, (void)rbits;
 #endif

@@ -31,7 +31,7 @@ import torch  # noqa: E402  (before libdpow: one shared HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import distpow  # noqa: E402
-from distpow.node import NodeResult, node_mine, node_mine_async, partition_of_rank  # noqa: E402
+from distpow.node import NodeBoard, NodeResult, node_mine, node_mine_async, partition_of_rank  # noqa: E402
 
 NONCE = [1, 2, 3, 4]
 SWEEP_NTZ = 32
@@ -45,6 +45,8 @@ TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first
 # the GPUs idle during it) unless DPOW_NODE_ASYNC=1 selects node_mine_async (ticked all-reduce
 # beside the running kernels, bound injection).
 NODE_SYNC = os.environ.get("DPOW_NODE_ASYNC") != "1"
+# N > 1: the node's shared-memory Found fan-out (NodeBoard) unless DPOW_NODE_BOARD=0
+NODE_BOARD = os.environ.get("DPOW_NODE_BOARD") != "0"
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
 # INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,
 # the MI355X_MICROARCH.md FP32 vector peak (157.3 TFLOP/s) / 2 FLOP per FMA lane-op.
@@ -71,6 +73,8 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: 2^38 candidates per step in total, split over the ranks "
                          "(default: weak, 2^36 per GPU)")
+    ap.add_argument("--no-dist", action="store_true",
+                    help="N = 1 without a (world-1) process group: no collective in the step")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank searches on device 0 (with --backend gloo)")
     args = ap.parse_args()
@@ -83,6 +87,7 @@ def main():
     device = 0 if args.same_device else local_rank
     torch.cuda.set_device(device)
     tick_group = None
+    dist_on = world > 1 or not args.no_dist
     if world > 1:
         if args.backend == "nccl":  # RCCL over xGMI
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
@@ -90,6 +95,17 @@ def main():
                 tick_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group("gloo")
+    elif dist_on:
+        # One GPU: a world-1 RCCL group all the same, so the N = 1 line runs the code path of
+        # the N-GPU node -- the per-step all-reduce and node_mine's batch boundaries over RCCL.
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                                    device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)
+    board = None
+    if world > 1 and NODE_BOARD:
+        board = NodeBoard.create()  # None when the ranks do not share one host
     wb, wbits = partition_of_rank(rank, world)
     R = 1 << (8 - wbits)
     per_gpu = (STRONG_TOTAL_PER_STEP // world) if args.strong else CANDIDATES_PER_GPU_PER_STEP
@@ -107,13 +123,13 @@ def main():
         k_begin = K0 + (s % n_windows) * batch_k
         r = miner.search(NONCE, SWEEP_NTZ, wb, wbits, k_begin, k_begin + batch_k)
         assert r.status == distpow.EXHAUSTED, r  # N = 32 is unreachable in 2^36 candidates
-        if world > 1:
+        if dist_on:
             red[0] = r.global_idx if r.status == distpow.FOUND else distpow.DPOW_NO_HIT
             red[1] = 1
             dist.all_reduce(red, op=dist.ReduceOp.MIN)
 
     def barrier():
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -133,7 +149,7 @@ def main():
     st = miner.stats()
     stream_ms = ev0.elapsed_time(ev1)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
@@ -145,36 +161,47 @@ def main():
     achieved_tops = cand_per_launch * OPS_PER_CANDIDATE / (avg_launch_ms * 1e-3) / 1e12
     kernel_ghs = st.candidates / (st.kernel_ms * 1e-3) / 1e9
 
-    # time-to-secret for the BASELINE configs (deterministic answers; node-wide when world > 1)
+    # time-to-secret for the BASELINE configs (deterministic answers; node-wide when world > 1):
+    # search_ms = the search call (what a worker reports), ms = bracketed by barrier + device
+    # synchronize (it also waits out launches still queued behind the hit)
     tts = {}
+    extra = {}
     ttsk = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8),
             ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5)]
     # BASELINE config 5: N = 9 on fresh 4-byte nonces seeded random.Random(416)
     ttsk += [(n, 9) for n in config5_fresh_nonces()]
     for nonce, n in ([] if args.no_tts else ttsk):
-        runs = []
+        runs, search_runs = [], []
         for _ in range(TTS_RUNS):
             barrier()
             t1 = time.perf_counter()
             if world == 1:  # one rank: the miner's own pipelined windows, no batch boundaries
                 r = miner.mine(nonce, n)
                 res = NodeResult(r.status, r.global_idx, r.secret, 0, 0)
-            elif NODE_SYNC:  # round 1's batch-synchronous node search
-                res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world, device=dev)
+            elif NODE_SYNC:  # batch-synchronous node search, Found fan-out through the node board
+                res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world, device=dev,
+                                board=board, attach_fn=miner.attach_node)
             else:  # no batch boundaries: ticked all-reduce + the node's best injected into each rank's search
                 res = node_mine_async(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
                                       bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
                                       device=dev, tick_group=tick_group)
+            search_runs.append((time.perf_counter() - t1) * 1e3)
             barrier()
             runs.append((time.perf_counter() - t1) * 1e3)
             assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
         tts[f"{bytes(nonce).hex()}/{n}"] = {"ms": round(sorted(runs)[len(runs) // 2], 3),
+                                            "search_ms": round(sorted(search_runs)[len(search_runs) // 2], 3),
                                             "first_ms": round(runs[0], 3), "global_idx": res.global_idx,
                                             "secret": list(res.secret)}
 
+    # The node's collective path at this world size: the batch boundary of node_mine
+    # (host -> device copy, RCCL MIN all-reduce, device -> host copy, synchronize), and
+    # node_mine over Miner.search for two BASELINE cases.
+    if dist_on and not args.no_tts:
+        extra["collective"] = collective_probe(miner, rank, world, dev, board, args.backend)
+
     # Secondary sweep: the whole L = 3 chunk segment, k in [2^16, 2^24),
     # one variable message word; and the early-exit latency of a Found/Cancel (worker.go:194,209).
-    extra = {}
     if not args.no_tts:
         barrier()
         miner.reset_stats()
@@ -263,7 +290,8 @@ def main():
             "valu_probe": probe,
             "time_to_secret": tts,
             "time_to_secret_node_search": ("one rank: Miner.mine" if world == 1 else
-                                           "node_mine (batch-synchronous)" if NODE_SYNC else
+                                           ("node_mine (batch-synchronous, node board)" if board is not None
+                                            else "node_mine (batch-synchronous)") if NODE_SYNC else
                                            "node_mine_async (ticked all-reduce, bound injection)"),
             **extra,
             "cpu_baseline": cpu,
@@ -272,8 +300,66 @@ def main():
         }
         print(json.dumps(out), flush=True)
     miner.close()
-    if world > 1:
+    if board is not None:
+        board.close()
+    if dist_on:
         dist.destroy_process_group()
+
+
+def collective_probe(miner, rank, world, dev, board, backend, reps=200):
+    """node_mine's batch boundary on this node's process group (RCCL with the nccl backend):
+    median us of [pinned host -> device copy, all-reduce MIN of 3 int64, device -> host
+    copy, stream synchronize] -- the per-batch cost c the expected-time batch of
+    node.auto_batch_candidates assumes -- and of one whole node_mine batch over a window
+    of 2^16 candidates per rank (the search call plus the boundary), and node_mine's
+    time-to-secret for two BASELINE cases over this group."""
+    on_gpu = dev.type == "cuda"
+    buf = torch.zeros(3, dtype=torch.int64, device=dev)
+    hbuf = torch.zeros(3, dtype=torch.int64, pin_memory=on_gpu)
+    lat = []
+    for i in range(reps + 10):
+        dist.barrier()
+        t = time.perf_counter()
+        hbuf[0], hbuf[1], hbuf[2] = i, 1, 1
+        if on_gpu:
+            buf.copy_(hbuf, non_blocking=True)
+        dist.all_reduce(buf if on_gpu else hbuf, op=dist.ReduceOp.MIN)
+        if on_gpu:
+            hbuf.copy_(buf, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+        _ = hbuf.tolist()
+        if i >= 10:
+            lat.append((time.perf_counter() - t) * 1e6)
+    wb, wbits = partition_of_rank(rank, world)
+    R = 1 << (8 - wbits)
+    search = lambda *a: miner.search(*a[:6], bound=a[6])  # noqa: E731
+    batch = []
+    for i in range(60):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        r = node_mine(search, NONCE, SWEEP_NTZ, rank, world, batch_k=(1 << 16) // R, k_start=K0 + i * (1 << 16) // R,
+                      k_limit=K0 + (i + 1) * (1 << 16) // R, device=dev)
+        if i >= 10:
+            batch.append((time.perf_counter() - t) * 1e6)
+        assert r.status == distpow.EXHAUSTED and r.batches == 1
+    tts = {}
+    for nonce, n in (([1, 2, 3, 4], 6), ([1, 2, 3, 4], 8)):
+        ms = []
+        for _ in range(TTS_RUNS):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            res = node_mine(search, nonce, n, rank, world, device=dev, board=board, attach_fn=miner.attach_node)
+            ms.append((time.perf_counter() - t) * 1e3)
+            assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
+        tts[f"{bytes(nonce).hex()}/{n}"] = {"search_ms": round(sorted(ms)[len(ms) // 2], 3),
+                                            "global_idx": res.global_idx, "batches": res.batches}
+    med = lambda v: round(sorted(v)[len(v) // 2], 1)  # noqa: E731
+    return {"backend": backend, "world": world,
+            "batch_boundary_us": {"median": med(lat), "p90": round(sorted(lat)[int(len(lat) * 0.9)], 1)},
+            "batch_2p16_candidates_us": {"median": med(batch), "p90": round(sorted(batch)[int(len(batch) * 0.9)], 1)},
+            "node_mine": tts}
 
 
 def coordinator_configs():

@@ -36,7 +36,6 @@ using namespace dpow;
 namespace {
 
 thread_local std::string g_last_error;
-thread_local bool g_slack_set = false;  // this thread's timer slack lowered (wait_record)
 
 int set_error(int code, const std::string &msg) {
     g_last_error = msg;
@@ -82,9 +81,22 @@ static_assert(kDepth < kClaimRing, "a claim slot is reused only after its launch
 constexpr size_t kRing = 8;  // completion records and event pairs, indexed by launch seq (>= kDepth + 1)
 // Word of the pinned cancel page holding the stale launch sequence (Launch::stale).
 constexpr size_t kStaleWord = 8;
-// Completion-record wait: spin this long (time-to-secret), then poll at kPollNs.
+// Completion-record wait: spin for the first kSpinNs of a search (time-to-secret),
+// then poll at kPollNs.
 constexpr int64_t kSpinNs = 200000;
 constexpr long kPollNs = 20000;
+constexpr int64_t kNoDeadline = INT64_MAX;
+// Deferred queueing.  A launch is queued only once the launches ahead of it are
+// expected to finish within kQueueLeadNs, so a hit leaves (almost) nothing queued
+// behind it: every queued launch of a persistent grid costs 10-20 us of dispatch
+// and retirement even when it claims nothing (profiles/r02_tts_timeline.json),
+// which the next search on the stream, and a device synchronize, wait out.  The
+// estimate is early on purpose (kEstRate is above every layout's measured rate,
+// the fixed cost below the measured one), so a window without a hit runs its
+// launches back to back.
+constexpr int64_t kQueueLeadNs = 60000;
+constexpr double kEstRate = 2.3e11;  // candidates/s of one device (bench: 217-218 on the one-block layouts)
+constexpr int64_t kEstFixedNs = 8000;
 
 // Searches in flight per device in this process.  Several logical workers may
 // share one GPU (the coordinator mirror places W workers round-robin on the
@@ -107,6 +119,35 @@ struct LaunchSlot {
     bool pending = false;  // events recorded, not yet harvested
     bool counted = false;  // its completion record was consumed: its work counts in the stats
     uint64_t candidates = 0;
+    uint64_t g_end = 0;    // global indices of this launch are below g_end = k_end * 256
+};
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// Per-search wait state: the search's start (the spin window), the caller thread's
+// timer slack (lowered for the sleeping polls, restored when the search returns --
+// the thread is the caller's own, e.g. a cgo goroutine's), and the node slot
+// (dpow_node_attach) as last seen.
+struct SearchWait {
+    int64_t t0 = now_ns();
+    long old_slack = -1;
+    uint64_t node_seen = DPOW_NO_HIT;  // lowest node best injected into this search
+    bool node_stop = false;            // the node slot's stop was seen
+    void lower_slack() {
+        if (old_slack >= 0) return;
+        // Linux pads a normal thread's nanosleep by its 50 us default timer slack,
+        // which a hit's record would wait out; 1 us keeps the poll at ~kPollNs.
+        const int r = prctl(PR_GET_TIMERSLACK, 0UL, 0UL, 0UL, 0UL);
+        if (r <= 0) return;
+        old_slack = r;
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+    }
+    ~SearchWait() {
+        if (old_slack >= 0) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)old_slack, 0UL, 0UL, 0UL);
+    }
 };
 
 }  // namespace
@@ -132,6 +173,9 @@ struct dpow_ctx {
     std::atomic<uint64_t> ext_bound{DPOW_NO_HIT};  // the lowest bound injected into the running search
     hipStream_t bound_stream = nullptr;
     hipEvent_t reset_ev = nullptr;
+    // Node slot (dpow_node_attach): shared by the ranks of one node, polled while a
+    // search waits for its records.
+    dpow_node_slot *node = nullptr;
 };
 
 namespace {
@@ -157,40 +201,247 @@ int harvest_all(dpow_ctx *c) {
     return 0;
 }
 
-// Wait for the completion record of launch `seq`.  Spins first (the record of
-// a launch holding a hit is the time-to-secret path), then sleeps between
+// Lower Ctrl::best of the running search to g (dpow_search_bound, and the node
+// slot's best): a one-thread atomicMin kernel on the bound stream, ordered after
+// the search's reset kernel.  The caller holds bound_mu.
+int inject_bound_locked(dpow_ctx *c, uint64_t g) {
+    if (g >= c->ext_bound.load(std::memory_order_relaxed)) return 0;
+    c->ext_bound.store(g, std::memory_order_release);
+    DPOW_HIP(hipSetDevice(c->device));
+    DPOW_HIP(hipStreamWaitEvent(c->bound_stream, c->reset_ev, 0));  // after this search's reset
+    const hipError_t e = search_bound(c->d_ctrl, g, c->bound_stream);
+    if (e != hipSuccess) return hip_fail(e, "search_bound");
+    return 0;
+}
+
+// The node slot, polled between record polls: a lower best of another rank is
+// injected as a bound; a stop marks every launch queued so far stale, so their
+// watchers stop them (the search then returns DPOW_CANCELLED).
+int poll_node(dpow_ctx *c, SearchWait &sw) {
+    dpow_node_slot *n = c->node;
+    if (!n) return 0;
+    const uint64_t nb = __atomic_load_n(&n->best, __ATOMIC_ACQUIRE);
+    if (nb < sw.node_seen) {
+        sw.node_seen = nb;
+        std::lock_guard<std::mutex> g(c->bound_mu);
+        const int rc = inject_bound_locked(c, nb);
+        if (rc < 0) return rc;
+    }
+    if (!sw.node_stop && __atomic_load_n(&n->stop, __ATOMIC_ACQUIRE) != 0u) {
+        sw.node_stop = true;
+        __atomic_store_n(&c->h_cancel[kStaleWord], (uint32_t)c->seq, __ATOMIC_RELEASE);
+    }
+    return 0;
+}
+
+// Wait for the completion record of launch `seq`, until `deadline` (now_ns()
+// clock; kNoDeadline: none).  Returns 1 when the record is there, 0 at the
+// deadline, < 0 on error.  Spins in the first kSpinNs of the search (the record
+// of a launch holding a hit is the time-to-secret path), then sleeps between
 // polls; the stream is queried now and then so a failed launch, or a stream
 // that went idle without writing the record, ends the wait with an error.
-int wait_record(dpow_ctx *c, uint64_t seq) {
+int wait_record(dpow_ctx *c, uint64_t seq, int64_t deadline, SearchWait &sw) {
     const uint32_t *p = &c->h_snap[seq % kRing].seq;
     const uint32_t want = (uint32_t)(seq + 1);
-    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t it = 1;; ++it) {
-        if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 0;
-        const int64_t ns =
-            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-        const bool spinning = ns < kSpinNs;
+        if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 1;
+        const int64_t t = now_ns();
+        if (t >= deadline) return 0;
+        const bool spinning = t - sw.t0 < kSpinNs;
         if (spinning ? (it % 4096 == 0) : (it % 16 == 0)) {
             const hipError_t q = hipStreamQuery(c->stream);
             if (q == hipSuccess) {
-                if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 0;
+                if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 1;
                 return set_error(DPOW_EHIP, "dpow_search: stream idle without the launch's completion record");
             }
             if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
         }
+        if (c->node && (!spinning || it % 64 == 0)) {
+            const int rc = poll_node(c, sw);
+            if (rc < 0) return rc;
+        }
         if (spinning) {
             __builtin_ia32_pause();
         } else {
-            // Linux pads a normal thread's nanosleep by its 50 us default timer slack,
-            // which a hit's record would wait out; 1 us keeps the poll at ~kPollNs.
-            if (!g_slack_set) {
-                (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
-                g_slack_set = true;
-            }
-            const struct timespec ts = {0, kPollNs};
+            sw.lower_slack();
+            int64_t ns = kPollNs;
+            if (deadline != kNoDeadline && deadline - t < ns) ns = deadline - t;
+            const struct timespec ts = {0, (long)ns};
             nanosleep(&ts, nullptr);
         }
     }
+}
+
+// The body of dpow_search (arguments checked).
+int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
+                  uint32_t worker_bits, uint64_t k_begin, uint64_t k_end, uint64_t *best_global_idx,
+                  uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len) {
+    WindowPlanner planner;
+    int rc = planner.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
+    if (rc < 0) return set_error(rc, "dpow_search: planning failed");
+    DPOW_HIP(hipSetDevice(c->device));
+    if (c->device >= kMaxDevices) return set_error(DPOW_EINVAL, "dpow_search: device ordinal too large");
+    const ActiveSearch active(c->device);
+    SearchWait sw;
+
+    {   // keep the stale mark within 2^30 launches of the present (int32 distance in the watcher)
+        uint32_t *st = &c->h_cancel[kStaleWord];
+        const uint32_t next = (uint32_t)(c->seq + 1);
+        if ((int32_t)(next - __atomic_load_n(st, __ATOMIC_RELAXED)) > (1 << 30))
+            __atomic_store_n(st, next - (1u << 30), __ATOMIC_RELAXED);
+    }
+    const uint64_t bound = *best_global_idx;
+    // Another rank's hit already on the node slot bounds this search from the start
+    // (as an injected bound: a record at or above it is not a hit of ours).
+    const uint64_t node_best = c->node ? __atomic_load_n(&c->node->best, __ATOMIC_ACQUIRE) : DPOW_NO_HIT;
+    sw.node_seen = node_best;
+    hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot),
+                                node_best < bound ? node_best : bound, c->stream, c->reset_ev);
+    if (e != hipSuccess) return hip_fail(e, "search_reset");
+    // Open the window for dpow_search_bound; closed (and its atomicMin kernels
+    // drained, so none lands on the next search's reset) on every return path.
+    struct BoundWindow {
+        dpow_ctx *c;
+        BoundWindow(dpow_ctx *cc, uint64_t start) : c(cc) {
+            std::lock_guard<std::mutex> g(c->bound_mu);
+            c->ext_bound.store(start, std::memory_order_relaxed);
+            c->searching = true;
+        }
+        ~BoundWindow() {
+            {
+                std::lock_guard<std::mutex> g(c->bound_mu);
+                c->searching = false;
+            }
+            (void)hipStreamSynchronize(c->bound_stream);
+        }
+    } bound_window(c, node_best);
+
+    const uint64_t seq0 = c->seq;
+    uint32_t done_target = 0;
+    size_t launched = 0, consumed = 0;
+    // Launches still queued when the search returns -- behind a hit, a bound, a
+    // cancel or an error -- are marked stale, so their watchers stop them at once
+    // even if the caller clears the cancel flag for its next task before they
+    // start.
+    struct StaleOnReturn {
+        dpow_ctx *c;
+        const size_t &launched, &consumed;
+        ~StaleOnReturn() {
+            if (consumed < launched) __atomic_store_n(&c->h_cancel[kStaleWord], (uint32_t)c->seq, __ATOMIC_RELEASE);
+        }
+    } stale_on_return{c, launched, consumed};
+    uint64_t best = bound;
+    int status = DPOW_EXHAUSTED;
+    // Consume the completion record of launch lj (in launch order): FOUND or
+    // CANCELLED ends the search, EXHAUSTED goes on, < 0 is an error.  Ctrl::best
+    // persists across the launches of a search and later launches hold higher
+    // indices, so the first record below the bound carries the answer.
+    auto consume = [&](size_t lj) -> int {
+        const uint64_t seq = seq0 + lj;
+        const int rc = wait_record(c, seq, kNoDeadline, sw);
+        if (rc < 0) return rc;
+        LaunchSlot &slot = c->slots[seq % kRing];
+        slot.counted = true;
+        consumed = lj + 1;
+        const Snap &sn = c->h_snap[seq % kRing];
+        if (sn.best < bound) {
+            // Ctrl::best = min(this search's hits, bounds injected by dpow_search_bound
+            // or from the node slot).  At or above the lowest injected bound it is not a
+            // hit of ours.  The search is over only when that bound lies within the
+            // launches consumed so far (every candidate below it has been searched);
+            // otherwise the later launches still hold candidates below it: go on
+            // (they skip chunks at or above Ctrl::best, and a hit of ours there shows
+            // in their records as a value below the bound).
+            const uint64_t eb = c->ext_bound.load(std::memory_order_acquire);
+            if (sn.best >= eb) return eb <= slot.g_end ? DPOW_BOUNDED : DPOW_EXHAUSTED;
+            best = sn.best;
+            return DPOW_FOUND;
+        }
+        if (sn.stop != 0u || sw.node_stop || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u)
+            return DPOW_CANCELLED;
+        return DPOW_EXHAUSTED;
+    };
+    int64_t busy_until = 0;  // expected end of the launches queued so far (now_ns clock)
+    PlannedLaunch pl;
+    bool have = planner.next(pl);
+    while (status == DPOW_EXHAUSTED && have) {
+        if (sw.node_stop) {
+            status = DPOW_CANCELLED;
+            break;
+        }
+        const size_t li = launched;
+        if (li - consumed >= kDepth) {  // the record of the oldest launch decides whether to go on
+            const int r = consume(consumed);
+            if (r < 0) return r;
+            if (r != DPOW_EXHAUSTED) status = r;
+            continue;
+        }
+        if (li > consumed && busy_until - now_ns() > kQueueLeadNs) {
+            // Deferred queueing: wait for the oldest record until the launches ahead
+            // are expected to be within kQueueLeadNs of their end.
+            const size_t lj = consumed;
+            const int w = wait_record(c, seq0 + lj, busy_until - kQueueLeadNs, sw);
+            if (w < 0) return w;
+            if (w == 1) {
+                const int r = consume(lj);
+                if (r < 0) return r;
+                if (r != DPOW_EXHAUSTED) status = r;
+                continue;
+            }
+        }
+        {   // a launch wholly at or above the bound (the caller's, an injected one) holds nothing
+            const uint64_t eb = c->ext_bound.load(std::memory_order_acquire);
+            if ((pl.info.k_begin << 8) >= (eb < bound ? eb : bound)) break;
+        }
+        const uint64_t seq = seq0 + li;
+        LaunchSlot &slot = c->slots[seq % kRing];
+        if (harvest(c, slot) < 0) return DPOW_EHIP;  // the slot's previous launch
+        Launch &L = pl.L;
+        // This search's share of the device's resident workgroups (1 / searches in flight on it).
+        const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
+        const uint64_t bpc = launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
+        const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * bpc / share, kClaimCounters);
+        uint64_t worker_blocks = 0;
+        rc = size_launch(pl, max_blocks, &worker_blocks);
+        if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
+        done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
+        L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
+        L.done_target = done_target;
+        L.ctrl = c->d_ctrl;
+        L.cancel = c->d_cancel;
+        L.stale = c->d_cancel + kStaleWord;
+        L.snap = c->d_snap + seq % kRing;
+        L.seq = (uint32_t)(seq + 1);
+        e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L, (uint32_t)(worker_blocks + 1),
+                          c->stream, slot.start, slot.end);
+        if (e != hipSuccess) return hip_fail(e, "search_launch");
+        slot.pending = true;
+        slot.counted = false;
+        slot.candidates = L.i_end - L.i_begin;
+        slot.g_end = pl.info.k_end << 8;
+        c->seq = seq + 1;
+        ++launched;
+        const int64_t t = now_ns();
+        busy_until = std::max(busy_until, t) + kEstFixedNs +
+                     (int64_t)((double)slot.candidates * (double)share / kEstRate * 1e9);
+        have = planner.next(pl);
+    }
+    while (status == DPOW_EXHAUSTED && consumed < launched) {  // the window is queued: drain in order
+        const int r = consume(consumed);
+        if (r < 0) return r;
+        status = r;
+    }
+    if (status == DPOW_BOUNDED) status = DPOW_EXHAUSTED;  // no hit below the (injected) bound
+
+    if (status == DPOW_FOUND) {
+        dpow_secret_from_index(best, secret_out, secret_len);
+        if (!dpow_verify(nonce, nonce_len, secret_out, *secret_len, ntz)) {
+            *secret_len = 0;
+            return set_error(DPOW_EVERIFY, "dpow_search: kernel hit failed host MD5 verification");
+        }
+        *best_global_idx = best;
+    }
+    return status;
 }
 
 }  // namespace
@@ -301,14 +552,31 @@ int dpow_search_bound(dpow_ctx *c, uint64_t global_idx) {
     if (!c) return set_error(DPOW_EINVAL, "dpow_search_bound: ctx is NULL");
     std::lock_guard<std::mutex> g(c->bound_mu);
     if (!c->searching) return 0;  // no search in flight: the caller passes its bound to the next one
-    uint64_t cur = c->ext_bound.load(std::memory_order_relaxed);
-    if (global_idx >= cur) return 0;
-    c->ext_bound.store(global_idx, std::memory_order_release);
-    DPOW_HIP(hipSetDevice(c->device));
-    DPOW_HIP(hipStreamWaitEvent(c->bound_stream, c->reset_ev, 0));  // after this search's reset
-    const hipError_t e = search_bound(c->d_ctrl, global_idx, c->bound_stream);
-    if (e != hipSuccess) return hip_fail(e, "search_bound");
+    return inject_bound_locked(c, global_idx);
+}
+
+int dpow_node_attach(dpow_ctx *c, dpow_node_slot *slot) {
+    if (!c) return set_error(DPOW_EINVAL, "dpow_node_attach: ctx is NULL");
+    c->node = slot;
     return 0;
+}
+
+void dpow_node_slot_reset(dpow_node_slot *slot) {
+    if (!slot) return;
+    __atomic_store_n(&slot->stop, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&slot->best, DPOW_NO_HIT, __ATOMIC_RELEASE);
+}
+
+void dpow_node_post(dpow_node_slot *slot, uint64_t global_idx) {
+    if (!slot) return;
+    uint64_t cur = __atomic_load_n(&slot->best, __ATOMIC_RELAXED);
+    while (global_idx < cur &&
+           !__atomic_compare_exchange_n(&slot->best, &cur, global_idx, true, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED)) {
+    }
+}
+
+void dpow_node_stop(dpow_node_slot *slot) {
+    if (slot) __atomic_store_n(&slot->stop, 1u, __ATOMIC_RELEASE);
 }
 
 int dpow_secret_from_index(uint64_t g, uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len) {
@@ -425,131 +693,21 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     *secret_len = 0;
     c->stats.searches++;
     if (k_begin >= k_end) return DPOW_EXHAUSTED;
-    if (__atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
-
-    WindowPlanner planner;
-    int rc = planner.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
-    if (rc < 0) return set_error(rc, "dpow_search: planning failed");
-    DPOW_HIP(hipSetDevice(c->device));
-    if (c->device >= kMaxDevices) return set_error(DPOW_EINVAL, "dpow_search: device ordinal too large");
-    const ActiveSearch active(c->device);
-
-    {   // keep the stale mark within 2^30 launches of the present (int32 distance in the watcher)
-        uint32_t *st = &c->h_cancel[kStaleWord];
-        const uint32_t next = (uint32_t)(c->seq + 1);
-        if ((int32_t)(next - __atomic_load_n(st, __ATOMIC_RELAXED)) > (1 << 30))
-            __atomic_store_n(st, next - (1u << 30), __ATOMIC_RELAXED);
+    // A node slot whose stop is raised (another rank was cancelled or failed), or a
+    // raised cancel flag: nothing to do.  A node slot's stop is raised by every
+    // attached rank that returns DPOW_CANCELLED or an error, so the other ranks end
+    // their searches too (node_stop below).
+    dpow_node_slot *const node = c->node;
+    if (node && __atomic_load_n(&node->stop, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
+    if (__atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) {
+        dpow_node_stop(node);
+        return DPOW_CANCELLED;
     }
-    const uint64_t bound = *best_global_idx;
-    hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot), bound, c->stream);
-    if (e != hipSuccess) return hip_fail(e, "search_reset");
-    DPOW_HIP(hipEventRecord(c->reset_ev, c->stream));
-    // Open the window for dpow_search_bound; closed (and its atomicMin kernels
-    // drained, so none lands on the next search's reset) on every return path.
-    struct BoundWindow {
-        dpow_ctx *c;
-        explicit BoundWindow(dpow_ctx *cc) : c(cc) {
-            std::lock_guard<std::mutex> g(c->bound_mu);
-            c->ext_bound.store(DPOW_NO_HIT, std::memory_order_relaxed);
-            c->searching = true;
-        }
-        ~BoundWindow() {
-            {
-                std::lock_guard<std::mutex> g(c->bound_mu);
-                c->searching = false;
-            }
-            (void)hipStreamSynchronize(c->bound_stream);
-        }
-    } bound_window(c);
-
-    const uint64_t seq0 = c->seq;
-    uint32_t done_target = 0;
-    size_t launched = 0, consumed = 0;
-    uint64_t best = bound;
-    int status = DPOW_EXHAUSTED;
-    // Consume the completion record of launch lj (in launch order): FOUND or
-    // CANCELLED ends the search, EXHAUSTED goes on, < 0 is an error.  Ctrl::best
-    // persists across the launches of a search and later launches hold higher
-    // indices, so the first record below the bound carries the answer.
-    auto consume = [&](size_t lj) -> int {
-        const uint64_t seq = seq0 + lj;
-        const int rc = wait_record(c, seq);
-        if (rc < 0) return rc;
-        c->slots[seq % kRing].counted = true;
-        consumed = lj + 1;
-        const Snap &sn = c->h_snap[seq % kRing];
-        if (sn.best < bound) {
-            // Ctrl::best = min(this search's hits, bounds injected by dpow_search_bound).
-            // At or above the lowest injected bound it is not a hit of ours: nothing
-            // below that bound remains in the window, so the search is over.
-            if (sn.best >= c->ext_bound.load(std::memory_order_acquire)) return DPOW_BOUNDED;
-            best = sn.best;
-            return DPOW_FOUND;
-        }
-        if (sn.stop != 0u || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
-        return DPOW_EXHAUSTED;
-    };
-    PlannedLaunch pl;
-    while (status == DPOW_EXHAUSTED && planner.next(pl)) {
-        const size_t li = launched;
-        if (li >= kDepth) {  // the record of launch li - kDepth decides whether to go on
-            const int r = consume(li - kDepth);
-            if (r < 0) return r;
-            if (r != DPOW_EXHAUSTED) {
-                status = r;
-                break;
-            }
-        }
-        const uint64_t seq = seq0 + li;
-        LaunchSlot &slot = c->slots[seq % kRing];
-        if (harvest(c, slot) < 0) return DPOW_EHIP;  // the slot's previous launch
-        Launch &L = pl.L;
-        // This search's share of the device's resident workgroups (1 / searches in flight on it).
-        const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
-        const uint64_t bpc = launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
-        const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * bpc / share, kClaimCounters);
-        uint64_t worker_blocks = 0;
-        rc = size_launch(pl, max_blocks, &worker_blocks);
-        if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
-        done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
-        L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
-        L.done_target = done_target;
-        L.ctrl = c->d_ctrl;
-        L.cancel = c->d_cancel;
-        L.stale = c->d_cancel + kStaleWord;
-        L.snap = c->d_snap + seq % kRing;
-        L.seq = (uint32_t)(seq + 1);
-        DPOW_HIP(hipEventRecord(slot.start, c->stream));
-        e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L, (uint32_t)(worker_blocks + 1),
-                          c->stream);
-        if (e != hipSuccess) return hip_fail(e, "search_launch");
-        DPOW_HIP(hipEventRecord(slot.end, c->stream));
-        slot.pending = true;
-        slot.counted = false;
-        slot.candidates = L.i_end - L.i_begin;
-        c->seq = seq + 1;
-        ++launched;
-    }
-    while (status == DPOW_EXHAUSTED && consumed < launched) {  // the window is queued: drain in order
-        const int r = consume(consumed);
-        if (r < 0) return r;
-        status = r;
-    }
-    if (status == DPOW_BOUNDED) status = DPOW_EXHAUSTED;  // no hit below the (injected) bound
-    if (status == DPOW_CANCELLED && consumed < launched) {
-        // Up to kDepth launches are still queued.  Mark them stale so their
-        // watchers stop them even when the caller clears the cancel flag for
-        // the context's next task before they start.
-        __atomic_store_n(&c->h_cancel[kStaleWord], (uint32_t)c->seq, __ATOMIC_RELEASE);
-    }
-
-    if (status == DPOW_FOUND) {
-        dpow_secret_from_index(best, secret_out, secret_len);
-        if (!dpow_verify(nonce, nonce_len, secret_out, *secret_len, ntz)) {
-            *secret_len = 0;
-            return set_error(DPOW_EVERIFY, "dpow_search: kernel hit failed host MD5 verification");
-        }
-        *best_global_idx = best;
+    const int status = search_window(c, nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end,
+                                     best_global_idx, secret_out, secret_len);
+    if (node) {
+        if (status == DPOW_FOUND) dpow_node_post(node, *best_global_idx);
+        else if (status != DPOW_EXHAUSTED) dpow_node_stop(node);
     }
     return status;
 }

@@ -3,10 +3,11 @@
 
 namespace dpow {
 
-hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream) {
+hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream,
+                         hipEvent_t start, hipEvent_t stop) {
     if (!variant_exists(nblk, w0, sh)) return hipErrorInvalidValue;
 #define DPOW_CASE(n, s) \
-    if (nblk == n && sh == s) return variant_launch_##n##_##s(w0, L, grid, stream);
+    if (nblk == n && sh == s) return variant_launch_##n##_##s(w0, L, grid, stream, start, stop);
     DPOW_CASE(1, 0) DPOW_CASE(1, 1) DPOW_CASE(1, 2) DPOW_CASE(1, 3)
     DPOW_CASE(2, 0) DPOW_CASE(2, 1) DPOW_CASE(2, 2) DPOW_CASE(2, 3)
 #undef DPOW_CASE

@@ -5,6 +5,8 @@
 #include "md5_search_kernel.h"
 #include "md5_variants.h"
 
+#include <hip/hip_ext.h>
+
 #ifndef DPOW_VNBLK
 #error "DPOW_VNBLK must be defined"
 #endif
@@ -50,10 +52,10 @@ KernelFn pick(int w0, bool eq) {
 #define DPOW_NAME(a, b, c) DPOW_CAT3(a, b, c)
 
 hipError_t DPOW_NAME(variant_launch_, DPOW_VNBLK, DPOW_VSH)(int w0, const Launch &L, uint32_t grid,
-                                                           hipStream_t stream) {
+                                                           hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
     KernelFn fn = pick(w0, use_d_equality(DPOW_VNBLK, L.ntz));
     if (!fn) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlockThreads), 0, stream, L);
+    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kBlockThreads), 0, stream, start, stop, 0, L);
     return hipGetLastError();
 }
 

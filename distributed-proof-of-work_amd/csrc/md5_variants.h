@@ -8,7 +8,8 @@
 namespace dpow {
 
 #define DPOW_DECL_VARIANT(n, s)                                                                  \
-    hipError_t variant_launch_##n##_##s(int w0, const Launch &L, uint32_t grid, hipStream_t st); \
+    hipError_t variant_launch_##n##_##s(int w0, const Launch &L, uint32_t grid, hipStream_t st, \
+                                        hipEvent_t start, hipEvent_t stop);                      \
     hipError_t variant_occupancy_##n##_##s(int w0, int *blocks_per_cu);
 DPOW_DECL_VARIANT(1, 0)
 DPOW_DECL_VARIANT(1, 1)
@@ -28,14 +29,18 @@ inline bool variant_exists(int nblk, int w0, int sh) {
     return false;
 }
 
-hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream);
+// start / stop (may be null): timing events recorded by the kernel's own dispatch
+// packet (hipExtLaunchKernel), not as separate marker packets between launches.
+hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream,
+                         hipEvent_t start, hipEvent_t stop);
 hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu);
 
 // Lower a running search's Ctrl::best to an external bound (search_ctrl.hip).
 hipError_t search_bound(Ctrl *ctrl, unsigned long long g, hipStream_t stream);
 
 // Per-search reset of the control block and claim counters (search_ctrl.hip).
+// done_ev (may be null) is recorded by the reset kernel's dispatch.
 hipError_t search_reset(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
-                        hipStream_t stream);
+                        hipStream_t stream, hipEvent_t done_ev);
 
 }  // namespace dpow

@@ -8,6 +8,8 @@
 #include "dpow_common.h"
 #include "md5_variants.h"
 
+#include <hip/hip_ext.h>
+
 namespace dpow {
 
 namespace {
@@ -34,8 +36,9 @@ hipError_t search_bound(Ctrl *ctrl, unsigned long long g, hipStream_t stream) {
 }
 
 hipError_t search_reset(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
-                        hipStream_t stream) {
-    hipLaunchKernelGGL(search_reset_kernel, dim3(1), dim3(kBlockThreads), 0, stream, ctrl, claims, n_claims, bound);
+                        hipStream_t stream, hipEvent_t done_ev) {
+    hipExtLaunchKernelGGL(search_reset_kernel, dim3(1), dim3(kBlockThreads), 0, stream, nullptr, done_ev, 0, ctrl,
+                          claims, n_claims, bound);
     return hipGetLastError();
 }
 

@@ -154,6 +154,10 @@ def lib():
         "dpow_search": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, u64p, u8p, szp]),
         "dpow_search_bound": (ctypes.c_int, [vp, ctypes.c_uint64]),
+        "dpow_node_attach": (ctypes.c_int, [vp, vp]),
+        "dpow_node_slot_reset": (None, [vp]),
+        "dpow_node_post": (None, [vp, ctypes.c_uint64]),
+        "dpow_node_stop": (None, [vp]),
         "dpow_secret_from_index": (ctypes.c_int, [ctypes.c_uint64, u8p, szp]),
         "dpow_md5": (None, [ctypes.c_char_p, ctypes.c_size_t, u8p]),
         "dpow_trailing_zero_nibbles": (ctypes.c_uint32, [ctypes.c_char_p]),

@@ -117,11 +117,15 @@ class Coordinator:
             return
         q.put(r)
 
-    def _get(self, q):
+    def _get(self, q, ack_phase: bool = False):
         try:
             r = q.get(timeout=self.timeout_s)
         except queue.Empty:
             raise CoordinatorProtocolError("timed out waiting for worker messages")
+        if r.error and ack_phase:
+            # The request already holds a verified secret: another worker's failed search
+            # is that worker's final message (recorded by _result), not a reason to fail it.
+            return r
         if r.error:
             # A failed GPU search (no counterpart in the Go reference, whose miner cannot
             # fail): surface it now rather than after timeout_s of waiting for ACKs.
@@ -156,26 +160,29 @@ class Coordinator:
             self._abort(key, nonce, ntz)
             raise
         if result.secret is None:
+            self._abort(key, nonce, ntz)
             raise CoordinatorProtocolError(
                 f"First worker result appears to be cancellation ACK, from workerByte = {result.worker_byte}")
         for w, wb in zip(self.workers, self.worker_bytes):
             self._record(tok, "CoordinatorWorkerCancel", Nonce=list(nonce), NumTrailingZeros=ntz, WorkerByte=wb)
             w.found(nonce, ntz, wb, result.secret, tok)
-        received = 1
-        extra = []
-        while received < 2 * W:
-            ack = self._get(q)
-            if ack.secret is not None:
-                extra.append(ack)
-            received += 1
-        for ack in extra:
-            for w, wb in zip(self.workers, self.worker_bytes):
-                self._record(tok, "CoordinatorWorkerCancel", Nonce=list(nonce), NumTrailingZeros=ntz, WorkerByte=wb)
-                w.found(nonce, ntz, wb, ack.secret, tok)
-            for _ in range(W):
-                self._get(q)
-        with self._tasks_mu:
-            del self._tasks[key]
+        try:
+            received = 1
+            extra = []
+            while received < 2 * W:
+                ack = self._get(q, ack_phase=True)
+                if ack.secret is not None:
+                    extra.append(ack)
+                received += 1
+            for ack in extra:
+                for w, wb in zip(self.workers, self.worker_bytes):
+                    self._record(tok, "CoordinatorWorkerCancel", Nonce=list(nonce), NumTrailingZeros=ntz, WorkerByte=wb)
+                    w.found(nonce, ntz, wb, ack.secret, tok)
+                for _ in range(W):
+                    self._get(q, ack_phase=True)
+        finally:
+            with self._tasks_mu:
+                self._tasks.pop(key, None)
         self._record(tok, "CoordinatorSuccess", Nonce=list(nonce), NumTrailingZeros=ntz, Secret=list(result.secret))
         return result.secret
 

@@ -22,7 +22,8 @@ from typing import Callable, Optional, Sequence
 
 from ._lib import CANCELLED, DPOW_K_LIMIT, DPOW_NO_HIT, EXHAUSTED, FOUND
 
-__all__ = ["NodeResult", "auto_batch_candidates", "node_mine", "node_mine_async", "partition_of_rank", "owner_rank"]
+__all__ = ["NodeResult", "NodeError", "NodeBoard", "auto_batch_candidates", "node_mine", "node_mine_async",
+           "partition_of_rank", "owner_rank"]
 
 
 @dataclass
@@ -73,10 +74,117 @@ def auto_batch_candidates(num_trailing_zeros: int, world: int, rate: float = RAN
     return int(min(hi, max(lo, b)))
 
 
+class NodeError(RuntimeError):
+    """Another rank's search failed: the node's search ends on every rank (the reference
+    log.Fatal's on a missing or malformed result, coordinator.go:202-206)."""
+
+
+class NodeBoard:
+    """The node's Found fan-out in shared memory (dpow_node_slot, include/dpow.h).
+
+    The ranks of one node map one small POSIX shared-memory segment of SLOTS 64-byte
+    slots.  node_mine uses slot (call index mod SLOTS) for one node search and attaches
+    it to the rank's GPU context: a rank's verified hit is posted to the slot at once,
+    and every other rank's running search takes it as its bound while it waits for its
+    kernels, so the node stops at its lowest hit without waiting for a batch boundary.
+    A cancelled or failed rank raises the slot's stop, which ends every rank's search.
+    The RCCL all-reduce at batch boundaries still decides the answer (the minimum over
+    the ranks, the workerBits = 0 first hit).  The slot of call c + 2 is reset at the
+    end of call c: every rank has passed call c + 1's last all-reduce before any rank
+    uses it, so no reset can race a post.
+
+    Created collectively (every rank of `group`); None from create() when the ranks do
+    not share one host (then node_mine runs on batch boundaries alone).
+    """
+    SLOTS = 4
+    SLOT_BYTES = 64
+
+    def __init__(self, shm, owner: bool):
+        import ctypes
+        self._shm = shm
+        self._owner = owner
+        self._base = ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+        self._calls = 0
+
+    @classmethod
+    def create(cls, group=None) -> Optional["NodeBoard"]:
+        import os
+        import socket
+        import uuid
+        from multiprocessing import shared_memory
+
+        import torch.distributed as dist
+
+        from ._lib import lib
+        me = (socket.gethostname(), open("/proc/sys/kernel/random/boot_id").read().strip())
+        world = dist.get_world_size(group)
+        hosts = [None] * world
+        dist.all_gather_object(hosts, me, group=group)
+        if any(h != me for h in hosts):
+            return None
+        rank = dist.get_rank(group)
+        name = [None]
+        shm = None
+        if rank == 0:
+            shm = shared_memory.SharedMemory(name=f"dpow_node_{os.getpid()}_{uuid.uuid4().hex[:12]}", create=True,
+                                             size=cls.SLOTS * cls.SLOT_BYTES)
+            name[0] = shm.name
+        dist.broadcast_object_list(name, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if rank != 0:
+            shm = shared_memory.SharedMemory(name=name[0])
+        board = cls(shm, rank == 0)
+        if rank == 0:
+            for i in range(cls.SLOTS):
+                lib().dpow_node_slot_reset(board.slot(i))
+        dist.barrier(group=group)
+        if rank == 0:  # every rank has it mapped: nothing is left in /dev/shm, whatever happens next
+            shm.unlink()
+        return board
+
+    def slot(self, i: int) -> int:
+        return self._base + (i % self.SLOTS) * self.SLOT_BYTES
+
+    def begin(self) -> int:
+        return self.slot(self._calls)
+
+    def end(self):
+        from ._lib import lib
+        lib().dpow_node_slot_reset(self.slot(self._calls + 2))
+        self._calls += 1
+
+    def best(self, slot: int) -> int:
+        import ctypes
+        return ctypes.c_uint64.from_address(slot).value
+
+    def stop(self, slot: int):
+        from ._lib import lib
+        lib().dpow_node_stop(slot)
+
+    def post(self, slot: int, global_idx: int):
+        from ._lib import lib
+        lib().dpow_node_post(slot, global_idx)
+
+    def close(self):
+        if self._shm is not None:
+            self._base = 0
+            try:
+                self._shm.close()
+            except BufferError:  # a ctypes view still alive; the mapping goes with the process
+                pass
+            self._shm = None
+
+
+# With a node board, hits end every rank's batch at once, so a batch costs its boundary
+# (the search call and the all-reduce) only when it holds no hit: batches can be long.
+BOARD_BATCH_CANDIDATES = 1 << 33
+
+
 def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
               batch_k: Optional[int] = None, k_start: int = 0, k_limit: int = DPOW_K_LIMIT, group=None,
               device=None, cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
-              batch_k_max: Optional[int] = None, batch_candidates_max: int = 1 << 29) -> NodeResult:
+              batch_k_max: Optional[int] = None, batch_candidates_max: int = 1 << 29,
+              board: Optional[NodeBoard] = None, attach_fn: Callable[[Optional[int]], None] = lambda s: None
+              ) -> NodeResult:
     """Search until the first hit of the whole node (deterministic) or a cancel vote.
 
     search_fn(nonce, ntz, worker_byte, worker_bits, k_begin, k_end, bound) -> SearchResult
@@ -85,62 +193,94 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
     Every rank must finish a batch before the all-reduce, so a batch bounds the
     overshoot past the hit, and each batch costs a fixed c on top of its hashing.
     - batch_k None (default): one constant batch per rank sized for N and the node
-      (auto_batch_candidates, the expected-time optimum of the geometric first hit).
+      (auto_batch_candidates, the expected-time optimum of the geometric first hit);
+      with a board, BOARD_BATCH_CANDIDATES (the board ends a batch at its first hit).
     - batch_k given: batches start at batch_k chunks and grow by `growth` up to
       batch_k_max (default: batch_candidates_max = 2^29 candidates per rank, 2.5 ms of
       hashing; 2^24 k at 8 GPUs).  For T ms of hashing per rank, c T / B + B / 2 is
       smallest near B = sqrt(2 c T), 2.3 ms for N = 9 at 8 GPUs.
+
+    The batch-boundary all-reduce runs whenever a process group is initialised (also at
+    world = 1): MIN over [best index, running, healthy].  A rank whose search raises
+    votes healthy = 0 in the same all-reduce, so no rank is left waiting in a collective
+    the failed rank never joins: the failing rank re-raises its error, the others raise
+    NodeError (coordinator.go:202-206: a missing result is fatal, not silent).
+
+    board / attach_fn: the node's shared-memory Found fan-out (NodeBoard); attach_fn(slot)
+    attaches a slot address to this rank's search context (Miner.attach_node), None
+    detaches.
     """
     import torch
     import torch.distributed as dist
 
     wb, wbits = partition_of_rank(rank, world)
     if batch_k is None:
-        batch_k = max(1, auto_batch_candidates(num_trailing_zeros, world) >> (8 - wbits % 9))
+        cand = BOARD_BATCH_CANDIDATES if board is not None else auto_batch_candidates(num_trailing_zeros, world)
+        batch_k = max(1, cand >> (8 - wbits % 9))
         growth = 1
     if batch_k_max is None:
         batch_k_max = max(1, batch_candidates_max >> (8 - wbits % 9))
-    dist_on = world > 1 and dist.is_available() and dist.is_initialized()
+    dist_on = dist.is_available() and dist.is_initialized()
     if device is None:
         backend = dist.get_backend(group) if dist_on else "gloo"
         device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    buf = torch.empty(2, dtype=torch.int64, device=device)
+    buf = torch.empty(3, dtype=torch.int64, device=device)
     # With a device buffer (RCCL), a pinned host twin carries the values in and out:
     # stream-ordered copies around the all-reduce and one stream synchronize per batch.
     on_gpu = buf.device.type == "cuda"
-    hbuf = torch.empty(2, dtype=torch.int64, pin_memory=True) if on_gpu else buf
+    hbuf = torch.empty(3, dtype=torch.int64, pin_memory=True) if on_gpu else buf
+    slot = board.begin() if board is not None else None
+    if slot is not None:
+        attach_fn(slot)
     bound = DPOW_NO_HIT
     secret = None
     k = k_start
     batches = 0
-    while k < k_limit:
-        ke = min(k_limit, k + batch_k)
-        batch_k = min(batch_k * growth, max(batch_k, batch_k_max))
-        r = search_fn(nonce, num_trailing_zeros, wb, wbits, k, ke, bound)
-        mine = r.global_idx if r.status == FOUND else DPOW_NO_HIT
-        if r.status == FOUND:
-            secret = r.secret
-        running = 0 if (r.status == CANCELLED or cancelled()) else 1
-        hbuf[0], hbuf[1] = mine, running
-        if on_gpu:
-            buf.copy_(hbuf, non_blocking=True)
-        if dist_on:
-            dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
-        if on_gpu:
-            hbuf.copy_(buf, non_blocking=True)
-            torch.cuda.current_stream(buf.device).synchronize()
-        batches += 1
-        best, all_running = (int(x) for x in hbuf.tolist())
-        if best != DPOW_NO_HIT:
-            own = owner_rank(best, world)
-            if best != mine:
-                secret = None  # another rank's partition won; its owner holds the secret bytes
-            from .search import secret_from_index
-            return NodeResult(FOUND, best, secret if secret is not None else secret_from_index(best), own, batches)
-        if not all_running:
-            return NodeResult(CANCELLED, batches=batches)
-        k = ke
-    return NodeResult(EXHAUSTED, batches=batches)
+    try:
+        while k < k_limit:
+            ke = min(k_limit, k + batch_k)
+            batch_k = min(batch_k * growth, max(batch_k, batch_k_max))
+            err = None
+            try:
+                r = search_fn(nonce, num_trailing_zeros, wb, wbits, k, ke, bound)
+            except Exception as e:  # voted below; re-raised after the all-reduce
+                err, r = e, None
+                if slot is not None:
+                    board.stop(slot)
+            found = r is not None and r.status == FOUND
+            mine = r.global_idx if found else DPOW_NO_HIT
+            if found:
+                secret = r.secret
+            running = 0 if (err is not None or r.status == CANCELLED or cancelled()) else 1
+            hbuf[0], hbuf[1], hbuf[2] = mine, running, 0 if err is not None else 1
+            if on_gpu:
+                buf.copy_(hbuf, non_blocking=True)
+            if dist_on:
+                dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
+            if on_gpu:
+                hbuf.copy_(buf, non_blocking=True)
+                torch.cuda.current_stream(buf.device).synchronize()
+            batches += 1
+            best, all_running, healthy = (int(x) for x in hbuf.tolist())
+            if not healthy:
+                if err is not None:
+                    raise err
+                raise NodeError(f"rank {rank}: another rank's search failed in batch {batches} "
+                                f"(k window [{k}, {ke}))")
+            if best != DPOW_NO_HIT:
+                own = owner_rank(best, world)
+                if best != mine:
+                    secret = None  # another rank's partition won; its owner holds the secret bytes
+                from .search import secret_from_index
+                return NodeResult(FOUND, best, secret if secret is not None else secret_from_index(best), own, batches)
+            if not all_running:
+                return NodeResult(CANCELLED, batches=batches)
+            k = ke
+        return NodeResult(EXHAUSTED, batches=batches)
+    finally:
+        if slot is not None:
+            attach_fn(None)
+            board.end()
 
 
 def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
@@ -195,7 +335,7 @@ def node_mine_async(search_fn: Callable, nonce: Sequence[int], num_trailing_zero
     if batch_k is None:
         batch_k = max(1, auto_batch_candidates(num_trailing_zeros, world) >> rbits)
     batch_k_max = max(1, batch_candidates_max >> rbits)
-    dist_on = world > 1 and dist.is_available() and dist.is_initialized()
+    dist_on = dist.is_available() and dist.is_initialized()
     if device is None:
         backend = dist.get_backend(group) if dist_on else "gloo"
         device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")

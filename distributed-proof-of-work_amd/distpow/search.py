@@ -144,6 +144,12 @@ class Miner:
         (dpow_search_bound).  No effect when no search runs."""
         check(lib().dpow_search_bound(self._ctx, global_idx), "dpow_search_bound")
 
+    def attach_node(self, slot: Optional[int]):
+        """Attach a node slot (NodeBoard.begin(): the address of a dpow_node_slot in the
+        node's shared memory) to this context's searches, or detach it (None)
+        (dpow_node_attach)."""
+        check(lib().dpow_node_attach(self._ctx, slot or None), "dpow_node_attach")
+
     @property
     def cancelled(self) -> bool:
         return self._cancel[0] != 0

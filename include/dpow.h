@@ -24,7 +24,10 @@
 extern "C" {
 #endif
 
-#define DPOW_ABI_VERSION 1
+/* 2: dpow_worker_result gained `error` (dpow_worker.h), DPOW_K_LIMIT = 2^55 - 1 and
+ * 7-byte chunks (round 2); dpow_node_* (round 3).  A consumer built against
+ * another version must refuse the library. */
+#define DPOW_ABI_VERSION 2
 
 /* "no hit" sentinel for global indices: INT64_MAX, so that signed (RCCL/gloo
  * int64 MIN) and unsigned (device atomicMin u64) reductions agree. */
@@ -102,6 +105,40 @@ int dpow_search(dpow_ctx *ctx, const uint8_t *nonce, size_t nonce_len, uint32_t 
  * coordinator.go:210-230, cancels instead).  No effect when no search runs.
  * Returns 0 or a negative error code. */
 int dpow_search_bound(dpow_ctx *ctx, uint64_t global_idx);
+
+/* ---------------------------------------------------------------------------
+ * Node slot (round 3): the Found fan-out of one node's ranks, in shared memory.
+ *
+ * The reference coordinator fans Found out to every worker once the first
+ * result arrives (coordinator.go:210-230).  Here the G GPUs of one node search
+ * the prefix partitions of the same k-window, one process each, and share a
+ * dpow_node_slot (e.g. a POSIX shared-memory page mapped by every rank).  A
+ * search on a context attached to a slot
+ *   - takes the slot's best as a bound from its start and whenever it drops
+ *     while the search waits for its launches (as dpow_search_bound), so every
+ *     rank stops at the node's lowest hit without waiting for a batch boundary;
+ *   - posts its own verified hit to the slot (atomic min) before it returns
+ *     DPOW_FOUND;
+ *   - returns DPOW_CANCELLED when the slot's stop is raised, and raises it when
+ *     it returns DPOW_CANCELLED or an error itself, so a cancelled or failed rank
+ *     ends the node's search on every GPU at once.
+ * The node's answer is still the minimum over the ranks' results (distpow.node:
+ * one RCCL MIN all-reduce per batch), which equals the workerBits = 0 first hit.
+ * ------------------------------------------------------------------------- */
+typedef struct dpow_node_slot {
+    uint64_t best;     /* lowest verified hit of any rank; DPOW_NO_HIT = none */
+    uint32_t stop;     /* non-zero: every attached search ends (DPOW_CANCELLED) */
+    uint32_t pad[13];  /* one 64-byte line per slot */
+} dpow_node_slot;
+/* Attach a slot to ctx for its next searches (NULL detaches).  Not thread-safe
+ * against a running search on ctx. */
+int dpow_node_attach(dpow_ctx *ctx, dpow_node_slot *slot);
+/* best = DPOW_NO_HIT, stop = 0 (before the node's search that uses the slot). */
+void dpow_node_slot_reset(dpow_node_slot *slot);
+/* Atomic min of a verified hit into the slot. */
+void dpow_node_post(dpow_node_slot *slot, uint64_t global_idx);
+/* Raise the slot's stop. */
+void dpow_node_stop(dpow_node_slot *slot);
 
 /* ---------------------------------------------------------------------------
  * Host helpers (no GPU needed).

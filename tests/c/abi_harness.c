@@ -59,6 +59,14 @@ int main(int argc, char **argv) {
     const int n = dpow_plan_window(nonce, sizeof nonce, 0, 0, 0, (1u << 24) + 5, plan, 8);
     if (n != 5 || plan[4].chunk_len != 4) return fail("dpow_plan_window");
     if (dpow_abi_version() != DPOW_ABI_VERSION) return fail("dpow_abi_version");
+    /* the node slot (host memory shared by a node's ranks): reset, post = atomic min, stop */
+    dpow_node_slot slot;
+    dpow_node_slot_reset(&slot);
+    dpow_node_post(&slot, 1000);
+    dpow_node_post(&slot, 2000);
+    if (slot.best != 1000 || slot.stop != 0 || sizeof slot != 64) return fail("dpow_node_post");
+    dpow_node_stop(&slot);
+    if (slot.stop == 0 || dpow_node_attach(NULL, &slot) != DPOW_EINVAL) return fail("dpow_node_stop");
     if (dpow_search(NULL, nonce, 4, 6, 0, 0, 0, 1, NULL, secret, &len) != DPOW_EINVAL) return fail("NULL ctx");
     if (sizeof(dpow_worker_result) != 56 + DPOW_MAX_NONCE) return fail("dpow_worker_result layout");
     const int gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;

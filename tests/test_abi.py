@@ -47,7 +47,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_device_count():
     import distpow
-    assert distpow.lib().dpow_abi_version() == 1
+    assert distpow.lib().dpow_abi_version() == 2
     assert distpow.device_count() >= 0
 
 
@@ -100,7 +100,7 @@ def test_c_abi_from_plain_c(tmp_path):
     distpow.lib()  # the build-id check
     out = subprocess.check_output([_build_c_harness(tmp_path)], timeout=60).decode()
     rec = json.loads(out)
-    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 1
+    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 2
 
 
 @pytest.mark.gpu

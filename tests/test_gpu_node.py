@@ -55,6 +55,24 @@ def _rank_main(rank, world, port, cases, out_q):
             r = node_mine_async(search, nonce, ntz, rank, world, bound_fn=m.bound, cancel_fn=m.cancel,
                                 clear_fn=m.clear_cancel)
             res.append(("async", r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner))
+        # the node board (the shared-memory Found fan-out, dpow_node_slot): each rank's
+        # context polls the slot, takes another rank's hit as its bound and posts its own
+        from distpow.node import NodeBoard
+        board = NodeBoard.create()
+        assert board is not None
+        for nonce, ntz in cases:
+            r = node_mine(search, nonce, ntz, rank, world, board=board, attach_fn=m.attach_node)
+            res.append(("board", r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner))
+        # a cancel on one rank through the board: its search returns CANCELLED and raises
+        # the slot's stop, which ends the other rank's search at once (not at a batch end)
+        if rank == 0:
+            threading.Timer(0.3, m.cancel).start()
+        t0 = time.perf_counter()
+        r = node_mine(search, [1, 2, 3, 4], 32, rank, world, batch_k=1 << 30, k_start=1 << 24, board=board,
+                      attach_fn=m.attach_node)
+        m.clear_cancel()
+        res.append(("board-cancel", r.status, r.batches, time.perf_counter() - t0))
+        board.close()
         # a real cancel on the last rank: its pinned flag stops its kernel mid-launch, the
         # search returns CANCELLED and the all-reduce's running slot stops every rank
         if rank == world - 1:
@@ -103,6 +121,14 @@ def test_node_mine_two_ranks_on_gpu(golden):
             assert tag == "async" and status == 1 and g == e["global_idx"] and secret == e["secret"], \
                 (rank, nonce, ntz, g)
             assert owner == (g & 0xFF) >> 7
+        for (nonce, ntz), (tag, status, g, secret, owner) in zip(cases, outs[rank][n + len(cases):n + 2 * len(cases)]):
+            e = exp[(tuple(nonce), ntz)]
+            assert tag == "board" and status == 1 and g == e["global_idx"] and secret == e["secret"], \
+                (rank, nonce, ntz, g)
+            assert owner == (g & 0xFF) >> 7
+        tag, status, batches, secs = outs[rank][-2]
+        # the batch (2^37 candidates per rank, > 1 s on a shared GPU) ends at the stop
+        assert tag == "board-cancel" and status == 2 and batches == 1 and secs < 1.0, outs[rank][-2]
         status, batches, secs = outs[rank][-1]
         assert status == 2, outs[rank][-1]  # CANCELLED on every rank
         assert secs < 5

@@ -6,6 +6,7 @@ count and worker partition.  Run on the GPU box:  pytest -m gpu
 """
 import hashlib
 import random
+import ctypes
 import threading
 import time
 
@@ -494,6 +495,76 @@ def test_search_bound_from_another_thread(miner, golden):
     miner.bound(5)  # no search in flight: no effect
     r = miner.search([1, 2, 3, 4], 6, 0, 0, 0, 1 << 30)
     assert r.status == FOUND and r.global_idx == e6["global_idx"]
+
+
+class _Slot(ctypes.Structure):
+    """dpow_node_slot (include/dpow.h)."""
+    _fields_ = [("best", ctypes.c_uint64), ("stop", ctypes.c_uint32), ("pad", ctypes.c_uint32 * 13)]
+
+
+def test_bound_beyond_a_chunk_length_split(miner, golden):
+    """a bound from another partition that lies past the launch being
+    consumed must not end the search -- later launches of the window (here the L = 3
+    segment after the L = 2 one: the window splits at k = 2^16) still hold candidates
+    below it, among them this search's own first hit.  The bound is the node slot's best
+    at the search's start (deterministic: the first launch's record already shows it)."""
+    e7 = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 7)
+    g7 = e7["global_idx"]  # k = 905,898: in the L = 3 launch of a window from k = 256
+    assert (g7 >> 8) > (1 << 16)
+    slot = _Slot()
+    lib = distpow.lib()
+    addr = ctypes.addressof(slot)
+    try:
+        miner.attach_node(addr)
+        for b, want in ((g7 + 1000, (FOUND, g7)),          # beyond launch 0's end, above our hit
+                        ((1 << 24) << 8, (FOUND, g7)),     # at the window's end
+                        (g7 - 1, (EXHAUSTED, None)),       # below our hit: nothing wanted
+                        (((1 << 16) - 7) << 8, (EXHAUSTED, None))):  # inside launch 0
+            lib.dpow_node_slot_reset(addr)
+            lib.dpow_node_post(addr, b)
+            r = miner.search([1, 2, 3, 4], 7, 0, 0, 256, 1 << 24)
+            assert (r.status, r.global_idx if r.status == FOUND else None) == want, (b, r)
+            # a hit is posted to the slot (atomic min); a bounded search leaves it alone
+            assert slot.best == (min(b, g7) if r.status == FOUND else b) and slot.stop == 0
+        # a raised stop: the search returns CANCELLED at once and does not hash
+        lib.dpow_node_slot_reset(addr)
+        lib.dpow_node_stop(addr)
+        t0 = time.perf_counter()
+        assert miner.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, 1 << 40).status == CANCELLED
+        assert time.perf_counter() - t0 < 0.05
+    finally:
+        miner.attach_node(None)
+    # detached: the same window finds the hit without any bound
+    r = miner.search([1, 2, 3, 4], 7, 0, 0, 256, 1 << 24)
+    assert r.status == FOUND and r.global_idx == g7
+
+
+def test_node_stop_ends_a_running_search(miner):
+    """The node slot's stop raised from another thread (another rank was cancelled or
+    failed) ends a running search within a fraction of a second: DPOW_CANCELLED."""
+    slot = _Slot()
+    addr = ctypes.addressof(slot)
+    lib = distpow.lib()
+    lib.dpow_node_slot_reset(addr)
+    miner.attach_node(addr)
+    try:
+        out = {}
+        th = threading.Thread(target=lambda: out.update(r=miner.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, 1 << 40),
+                                                       t=time.perf_counter()))
+        th.start()
+        time.sleep(0.3)
+        t0 = time.perf_counter()
+        lib.dpow_node_stop(addr)
+        th.join(timeout=30)
+        assert not th.is_alive() and out["r"].status == CANCELLED
+        lat = out["t"] - t0
+        assert lat < 0.25, lat
+        print(f"node stop -> return {lat * 1e3:.2f} ms")
+    finally:
+        miner.attach_node(None)
+    # nothing leaks into the next search (stale launches stopped, flag untouched)
+    r = miner.search([1, 2, 3, 4], 6, 0, 0, 0, 1 << 30)
+    assert r.status == FOUND
 
 
 def test_concurrent_searches_share_the_gpu(golden):

@@ -190,3 +190,152 @@ def test_node_mine_default_schedule_gloo(golden):
             assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, nonce, ntz)
             assert owner == (g & 0xFF) >> 7
     assert [r[4] for r in outs[0]] == [r[4] for r in outs[1]]
+
+
+class _Injected(RuntimeError):
+    pass
+
+
+def _worker_fail(rank, world, port, out_q, fail_rank, use_board):
+    """One rank's search raises at its third batch (a failed GPU search, an EVERIFY, a
+    lost device): every rank must leave node_mine within seconds -- the failing one with
+    its own error, the others with NodeError -- instead of waiting in an all-reduce."""
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+    import torch.distributed as dist
+    from distpow.node import NodeBoard, NodeError, node_mine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    board = NodeBoard.create() if use_board else None
+    fn = _oracle_search_fn()
+    calls = {"n": 0}
+
+    def search(*a):
+        calls["n"] += 1
+        if rank == fail_rank and calls["n"] == 3:
+            raise _Injected("injected search failure")
+        return fn(*a)
+
+    t0 = time.perf_counter()
+    try:
+        node_mine(search, [1, 2, 3, 4], 32, rank, world, batch_k=16, k_limit=1 << 20, board=board)
+        out = ("returned",)
+    except _Injected:
+        out = ("own-error",)
+    except NodeError:
+        out = ("node-error",)
+    out_q.put((rank, out + (calls["n"], time.perf_counter() - t0)))
+    # the node is still usable afterwards: the next search runs in step on every rank
+    r = node_mine(fn, [1, 2, 3, 4], 3, rank, world, batch_k=64, board=board)
+    out_q.put((rank, ("next", r.status, r.global_idx)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("use_board", [False, True])
+def test_failing_rank_stops_the_node(use_board):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_fail, args=(r, world, port, q, 1, use_board)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(2 * world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    first = {r: o for r, o in got if o[0] != "next"}
+    nxt = {r: o for r, o in got if o[0] == "next"}
+    assert first[1][0] == "own-error" and first[0][0] == "node-error", first
+    assert first[0][1] == first[1][1] == 3  # both left at the failing batch
+    assert all(o[-1] < 5.0 for o in first.values()), first
+    assert nxt[0] == nxt[1] == ("next", 1, 97)  # config 1's answer, [1,2,3,4]/3 -> idx 97
+
+
+def _worker_board(rank, world, port, cases, out_q):
+    """node_mine with a NodeBoard over gloo.  Each rank's search (the oracle) takes the
+    slot's best as its bound when it starts and posts its hit, as dpow_search does for an
+    attached context; the answers must stay the workerBits = 0 goldens over many
+    consecutive searches (the slots cycle and are reset two calls ahead)."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+    import torch.distributed as dist
+    from distpow import search as S
+    from distpow.node import NodeBoard, node_mine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    board = NodeBoard.create()
+    assert board is not None  # one host
+    fn = _oracle_search_fn()
+    att = {"slot": None, "attached": 0}
+
+    def attach(slot):
+        att["slot"] = slot
+        att["attached"] += slot is not None
+
+    def search(nonce, ntz, wb, wbits, k0, k1, bound):
+        slot = att["slot"]
+        r = fn(nonce, ntz, wb, wbits, k0, k1, min(bound, board.best(slot)))
+        if r.status == S.FOUND:
+            board.post(slot, r.global_idx)
+        return r
+
+    res = []
+    for _ in range(3):
+        for nonce, ntz in cases:
+            r = node_mine(search, nonce, ntz, rank, world, batch_k=64, board=board, attach_fn=attach)
+            res.append((r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner))
+    assert att["slot"] is None and att["attached"] == 3 * len(cases)
+    board.close()
+    out_q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_node_board_gloo_matches_wbits0_answer(golden):
+    world = 2
+    cases = [(e["nonce"], e["ntz"]) for e in golden["first_hits"] if e["global_idx"] < 200_000]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_board, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = {(tuple(e["nonce"]), e["ntz"]): e for e in golden["first_hits"]}
+    for rank in range(world):
+        for (nonce, ntz), (status, g, secret, owner) in zip(cases * 3, outs[rank]):
+            e = exp[(tuple(nonce), ntz)]
+            assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, nonce, ntz)
+            assert owner == (g & 0xFF) >> 7
+
+
+def test_node_mine_world1_group_runs_the_collective():
+    """At world 1 with a process group, node_mine takes the collective path (the same code
+    the N-GPU node runs), here over gloo on the CPU."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import torch.distributed as dist
+    from distpow.node import node_mine
+    port = _free_port()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    calls = []
+    orig = dist.all_reduce
+
+    def spy(*a, **k):
+        calls.append(a[0].tolist())
+        return orig(*a, **k)
+    dist.all_reduce = spy
+    try:
+        r = node_mine(_oracle_search_fn(), [1, 2, 3, 4], 3, 0, 1, batch_k=64)
+    finally:
+        dist.all_reduce = orig
+        dist.destroy_process_group()
+    assert r.status == 1 and r.global_idx == 97 and r.owner == 0
+    assert calls == [[97, 1, 1]]

@@ -99,12 +99,24 @@ class NodeBoard:
     SLOTS = 4
     SLOT_BYTES = 64
 
-    def __init__(self, shm, owner: bool):
+    def __init__(self, shm=None):
         import ctypes
         self._shm = shm
-        self._owner = owner
-        self._base = ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+        if shm is not None:
+            self._base = ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+        else:  # local(): one process's own slots (single-rank use, tools/node_probe.py)
+            self._mem = (ctypes.c_uint64 * (self.SLOTS * self.SLOT_BYTES // 8))()
+            self._base = ctypes.addressof(self._mem)
         self._calls = 0
+
+    @classmethod
+    def local(cls) -> "NodeBoard":
+        """A board in this process's memory (no other rank can map it)."""
+        from ._lib import lib
+        board = cls()
+        for i in range(cls.SLOTS):
+            lib().dpow_node_slot_reset(board.slot(i))
+        return board
 
     @classmethod
     def create(cls, group=None) -> Optional["NodeBoard"]:
@@ -132,7 +144,7 @@ class NodeBoard:
         dist.broadcast_object_list(name, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         if rank != 0:
             shm = shared_memory.SharedMemory(name=name[0])
-        board = cls(shm, rank == 0)
+        board = cls(shm)
         if rank == 0:
             for i in range(cls.SLOTS):
                 lib().dpow_node_slot_reset(board.slot(i))
@@ -252,7 +264,11 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
             if found:
                 secret = r.secret
             running = 0 if (err is not None or r.status == CANCELLED or cancelled()) else 1
-            hbuf[0], hbuf[1], hbuf[2] = mine, running, 0 if err is not None else 1
+            # The board's best is another rank's verified hit in this same batch (one slot per
+            # node search): voting it too ends the batch for a rank that was bounded by it even
+            # without a process group, and the all-reduce's minimum is unchanged.
+            vote = min(mine, board.best(slot)) if slot is not None else mine
+            hbuf[0], hbuf[1], hbuf[2] = vote, running, 0 if err is not None else 1
             if on_gpu:
                 buf.copy_(hbuf, non_blocking=True)
             if dist_on:

@@ -1,21 +1,29 @@
 #!/usr/bin/env python3
-"""Time-to-secret of node_mine's batch schedules, one rank emulated on one GPU.
+"""Time-to-secret of a G-GPU node, emulated rank by rank on one GPU.
 
-    python tools/node_probe.py [runs]
+    python tools/node_probe.py [runs] > profiles/<round>_node_probe.json
 
-For a node of G GPUs the time to the answer is the time the rank owning the answer
-(owner = (g & 255) >> (8 - log2 G)) takes to reach it: its own first hit is the node's
-answer (the min rule), and the other ranks only have to finish the same batches.  This
-runs that rank alone (world = G, no process group: no all-reduce, but the per-batch
-host <-> device copies of the all-reduce buffer do run) for the bench's time-to-secret
-configs, with the growing schedule (2^8 k, x4, cap 2^29 candidates; round 2's first) and
-the expected-time schedule (node.auto_batch_candidates).  It also measures the fixed
-per-batch cost c of this loop (tiny batches at N = 32).  An 8-GPU node adds one RCCL
-all-reduce of 16 bytes per batch on top.
+node_mine with the node board (NodeBoard: the shared-memory Found fan-out,
+dpow_node_slot): every rank searches its partition of the same window; the rank that
+owns the answer (owner = (g & 255) >> (8 - log2 G)) posts it to the board the moment
+its search returns, and every other rank's running search takes it as its bound and
+stops.  The node's time is therefore the slowest rank's: the owner's time to its own
+hit, or a non-owner's time to notice the posted hit and drain.  This runs
+
+  1. the owner alone (world = G, no process group): t_owner;
+  2. every other rank alone, with a thread that posts the owner's hit to the board
+     slot t_owner after the rank's search started (as the owner's process would);
+
+and reports max over ranks, next to one GPU's Miner.mine (G1) and the world-1 RCCL
+batch boundary (pinned copy + all-reduce + copy + synchronize), which the real node
+adds once per batch (one batch, at these N).  The ranks run one after another, each
+with the whole GPU, so this is the node's time without its RCCL collective; the
+8-GPU number itself is the driver's (bench.py --gpus 8).
 """
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -24,7 +32,11 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-proof-of-work_amd"))
 import torch  # noqa: E402
 
 import distpow  # noqa: E402
-from distpow.node import auto_batch_candidates, node_mine, owner_rank  # noqa: E402
+from distpow.node import NodeBoard, node_mine, owner_rank  # noqa: E402
+
+
+def med(v):
+    return round(sorted(v)[len(v) // 2], 3)
 
 
 def main():
@@ -35,61 +47,74 @@ def main():
     exp = {(tuple(e["nonce"]), e["ntz"]): e["global_idx"] for e in gold["first_hits"] + gold["deep_hits"]}
     want += [(list(n), 9) for (n, z) in exp if z == 9 and n not in ((1, 2, 3, 4), (5, 6, 7, 8), (2, 2, 2, 2))]
     dev = torch.device("cuda", 0)
-    out = {"per_batch_cost_ms": {}, "tts_ms": {}}
+    out = {"note": __doc__.strip().splitlines()[0], "g1_ms": {}, "node_ms": {}}
+    board = NodeBoard.local()
+    lib = distpow.lib()
     with distpow.Miner(0) as m:
         search = lambda *a: m.search(*a[:6], bound=a[6])  # noqa: E731
         m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 26))  # warm
-        for G in (1, 8):
-            nb = 200
-            t = time.perf_counter()
-            r = node_mine(search, [1, 2, 3, 4], 32, 0, G, batch_k=1 << 6, growth=1, k_start=1 << 24,
-                          k_limit=(1 << 24) + nb * (1 << 6), device=dev)
-            assert r.status == distpow.EXHAUSTED and r.batches == nb
-            out["per_batch_cost_ms"][f"G{G}"] = round((time.perf_counter() - t) * 1e3 / nb, 4)
-        for G in (1, 2, 4, 8):
+        for nonce, n in want:
+            ts = []
+            for _ in range(runs):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                r = m.mine(nonce, n)
+                ts.append((time.perf_counter() - t) * 1e3)
+                assert r.global_idx == exp[(tuple(nonce), n)]
+            out["g1_ms"][f"{bytes(nonce).hex()}/{n}"] = med(ts)
+
+        def run_rank(nonce, n, rank, G, post_after_s=None, g=None):
+            slot = board.begin()
+            stop = threading.Event()
+
+            def poster(t0):
+                while time.perf_counter() - t0 < post_after_s and not stop.is_set():
+                    pass
+                lib.dpow_node_post(slot, g)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            th = None
+            if post_after_s is not None:
+                th = threading.Thread(target=poster, args=(t0,))
+                th.start()
+            res = node_mine(search, nonce, n, rank, G, device=dev, board=board, attach_fn=m.attach_node)
+            dt = time.perf_counter() - t0
+            stop.set()
+            if th:
+                th.join()
+            return res, dt
+
+        for G in (2, 4, 8):
             for nonce, n in want:
                 g = exp[(tuple(nonce), n)]
                 o = owner_rank(g, G)
-                row = {"global_idx": g, "owner": o,
-                       "auto_batch_candidates": auto_batch_candidates(n, G)}
-                for name, kw in (("grow", {"batch_k": 1 << 8}), ("auto", {})):
-                    ts, nb = [], 0
-                    for _ in range(runs):
-                        torch.cuda.synchronize()
-                        t = time.perf_counter()
-                        r = node_mine(search, nonce, n, o, G, device=dev, **kw)
-                        ts.append((time.perf_counter() - t) * 1e3)
-                        assert r.status == distpow.FOUND and r.global_idx == g, (nonce, n, G, name, r)
-                        nb = r.batches
-                    row[name] = {"ms": round(sorted(ts)[len(ts) // 2], 3), "batches": nb}
-                out["tts_ms"][f"G{G} {bytes(nonce).hex()}/{n}"] = row
-                print(f"G{G} {bytes(nonce).hex()}/{n}: grow {row['grow']['ms']} ms ({row['grow']['batches']} b), "
-                      f"auto {row['auto']['ms']} ms ({row['auto']['batches']} b)", file=sys.stderr, flush=True)
-        # Every rank of the node (sync schedule): a rank hashes its batches up to and
-        # including the one that holds the answer, or stops at its own first hit in it;
-        # the node's time is the slowest rank's (plus one all-reduce per batch).
-        out["node_ms"] = {}
-        for G in (2, 8):
-            for nonce, n in want:
-                g = exp[(tuple(nonce), n)]
-                rb = 8 - (G.bit_length() - 1)
-                bk = max(1, auto_batch_candidates(n, G) >> rb)
-                k_lim = ((g >> 8) // bk + 1) * bk
+                t_own = []
+                for _ in range(runs):
+                    res, dt = run_rank(nonce, n, o, G)
+                    assert res.status == distpow.FOUND and res.global_idx == g, (nonce, n, G, res)
+                    t_own.append(dt)
+                t_o = sorted(t_own)[len(t_own) // 2]
                 per_rank = []
                 for r in range(G):
+                    if r == o:
+                        per_rank.append(round(t_o * 1e3, 3))
+                        continue
                     ts = []
                     for _ in range(runs):
-                        torch.cuda.synchronize()
-                        t = time.perf_counter()
-                        res = node_mine(search, nonce, n, r, G, device=dev, k_limit=k_lim)
-                        ts.append((time.perf_counter() - t) * 1e3)
-                        assert res.status in (distpow.FOUND, distpow.EXHAUSTED)
-                        assert res.status != distpow.FOUND or res.global_idx >= g
-                    per_rank.append(round(sorted(ts)[len(ts) // 2], 3))
+                        res, dt = run_rank(nonce, n, r, G, post_after_s=t_o, g=g)
+                        # bounded by the posted hit (EXHAUSTED of this rank's batch -> no
+                        # process group: node_mine reports the rank's own status), never a
+                        # hit above it
+                        assert res.status in (distpow.FOUND, distpow.EXHAUSTED), res
+                        assert res.status != distpow.FOUND or res.global_idx == g
+                        ts.append(dt * 1e3)
+                    per_rank.append(med(ts))
                 key = f"G{G} {bytes(nonce).hex()}/{n}"
-                out["node_ms"][key] = {"max_rank_ms": max(per_rank), "owner_ms": per_rank[owner_rank(g, G)],
-                                       "per_rank_ms": per_rank}
-                print(f"node {key}: slowest rank {max(per_rank)} ms, owner {per_rank[owner_rank(g, G)]} ms",
+                g1 = out["g1_ms"][f"{bytes(nonce).hex()}/{n}"]
+                out["node_ms"][key] = {"global_idx": g, "owner": o, "owner_ms": per_rank[o],
+                                       "max_rank_ms": max(per_rank), "per_rank_ms": per_rank,
+                                       "speedup_vs_g1": round(g1 / max(per_rank), 2)}
+                print(f"{key}: slowest rank {max(per_rank)} ms, owner {per_rank[o]} ms, G1 {g1} ms",
                       file=sys.stderr, flush=True)
     out["build_id"] = distpow.build_id()
     print(json.dumps(out, indent=1))

@@ -13,7 +13,7 @@ import torch  # noqa: E402,F401
 
 import distpow  # noqa: E402
 
-cases = [([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([2, 2, 2, 2], 8), ([1, 2, 3, 4], 8)]
+cases = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([2, 2, 2, 2], 8), ([1, 2, 3, 4], 8)]
 out = []
 with distpow.Miner(0) as m:
     m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 26))  # warm

@@ -402,7 +402,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         const uint64_t bpc = launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
         const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * bpc / share, kClaimCounters);
         uint64_t worker_blocks = 0;
-        rc = size_launch(pl, max_blocks, &worker_blocks);
+        rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), &worker_blocks);
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
@@ -641,7 +641,7 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
     size_t n = 0;
     while (planner.next(pl)) {
         uint64_t wblocks = 0;
-        const int r = size_launch(pl, max_blocks, &wblocks);
+        const int r = size_launch(pl, max_blocks, ~0ull, &wblocks);
         if (r < 0) return set_error(r, "dpow_diag_launch_geometry: launch grid leaves a claim counter without waves");
         if (out && n < max_launches) {
             dpow_diag_launch &d = out[n];

@@ -152,13 +152,29 @@ void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words
     }
 }
 
-int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks_out) {
+uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits) {
+    // A candidate passes with p = 16^-N (MD5's nibbles are uniform): the first hit of a
+    // partition is geometric with mean 16^N R / 256 of its candidates, from any start.
+    if (ntz >= 14) return ~0ull;
+    return ((1ull << (4 * ntz)) << rbits) >> 8;
+}
+
+int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks_out) {
     Launch &L = pl.L;
     constexpr uint64_t wpb = kBlockThreads / 64;
-    // Chunk: >= kClaimsPerWave claims per wave of the largest grid the launch gets.
+    // Chunk: >= kClaimsPerWave claims per wave of the largest grid the launch gets, over
+    // the launch -- or over the candidates before its expected first hit, when that is
+    // sooner.  A wave hashes its claims in order, and the chunks claimed first (a wave's
+    // current one and the one it claimed ahead) are held by every wave from the start,
+    // the youngest waves of a SIMD progressing slowest until the launch drains: a hit
+    // inside them waits for that.  A 537M-candidate launch (L = 3 at workerBits 3) with
+    // its N = 7 hit 29M in took 1.44 ms at chunk 32, against 0.31 ms for the same hit
+    // in a 36M-candidate launch at chunk 4 (profiles/r03_node_probe.json).
     uint64_t worker_blocks = (L.n_wblocks + wpb - 1) / wpb;
     if (worker_blocks > max_blocks) worker_blocks = max_blocks;
-    uint64_t chunk = L.n_wblocks / (worker_blocks * wpb * kClaimsPerWave);
+    uint64_t span_wb = L.n_wblocks;
+    if (expect / (uint64_t)kWaveBlock < span_wb) span_wb = expect / (uint64_t)kWaveBlock;
+    uint64_t chunk = span_wb / (worker_blocks * wpb * kClaimsPerWave);
     if (chunk < kMinChunk) chunk = kMinChunk;
     if (chunk > kMaxChunk) chunk = kMaxChunk;
     if (DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) {
@@ -203,8 +219,7 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks_
 uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits) {
 #if DPOW_SMALL_GRIDS
     // Candidates of this partition expected before its first hit: 16^N R / 256.
-    uint64_t expect = ~0ull;
-    if (ntz < 14) expect = ((1ull << (4 * ntz)) << rbits) >> 8;
+    const uint64_t expect = expected_first_hit(ntz, rbits);
     const uint64_t eff = candidates < expect ? candidates : expect;
     if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
     if (eff <= (1ull << 24)) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;

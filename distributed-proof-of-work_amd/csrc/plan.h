@@ -69,7 +69,11 @@ constexpr uint64_t kTailChunk = DPOW_TAIL_CHUNK;
 static_assert((kMinChunk & (kMinChunk - 1)) == 0 && (kMaxChunk & (kMaxChunk - 1)) == 0 &&
                   (kTailChunk & (kTailChunk - 1)) == 0 && kTailChunk <= kMinChunk,
               "chunk bounds are powers of two (segment alignment)");
-int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t *worker_blocks);
+// expect: candidates of the launch expected before its first hit (expected_first_hit;
+// ~0 = none): chunks are sized so that >= kClaimsPerWave claims per wave come before it.
+int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks);
+// Mean number of a partition's candidates before its first hit at N trailing zeros.
+uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits);
 
 // Worker workgroups per CU for one launch (before the device share).  The full
 // persistent grid (kMaxBlocksPerCu = 6) has the highest rate, but a launch that is

@@ -12,6 +12,7 @@
 // against Ctrl::best / Ctrl::stop before hashing), in stream order ahead of
 // the next search on the context.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/prctl.h>
 #include <time.h>
@@ -82,9 +83,10 @@ constexpr size_t kRing = 8;  // completion records and event pairs, indexed by l
 // Word of the pinned cancel page holding the stale launch sequence (Launch::stale).
 constexpr size_t kStaleWord = 8;
 // Completion-record wait: spin for the first kSpinNs of a search (time-to-secret),
-// then poll at kPollNs.
+// then poll at kPollNs (20 us in round 2: a record waited up to that long to be seen,
+// profiles/r03_stop_latency.json; the thread sleeps between polls either way).
 constexpr int64_t kSpinNs = 200000;
-constexpr long kPollNs = 20000;
+constexpr long kPollNs = 5000;
 constexpr int64_t kNoDeadline = INT64_MAX;
 // Deferred queueing.  A launch is queued only once the launches ahead of it are
 // expected to finish within kQueueLeadNs, so a hit leaves (almost) nothing queued
@@ -176,6 +178,9 @@ struct dpow_ctx {
     // Node slot (dpow_node_attach): shared by the ranks of one node, polled while a
     // search waits for its records.
     dpow_node_slot *node = nullptr;
+    dpow_node_slot *d_node = nullptr;  // its device alias (the watcher polls it)
+    std::vector<void *> registered;    // host pages registered for the node slots attached so far
+    uint32_t poll_override = 0;  // DPOW_DIAG_POLL_WB (A/B runs): wave-blocks per poll group for every launch
 };
 
 namespace {
@@ -222,10 +227,12 @@ int poll_node(dpow_ctx *c, SearchWait &sw) {
     if (!n) return 0;
     const uint64_t nb = __atomic_load_n(&n->best, __ATOMIC_ACQUIRE);
     if (nb < sw.node_seen) {
+        // The running launch's watcher lowers Ctrl::best to it on the device; the host
+        // keeps the injected bound (ext_bound) that tells another rank's index from ours.
         sw.node_seen = nb;
         std::lock_guard<std::mutex> g(c->bound_mu);
-        const int rc = inject_bound_locked(c, nb);
-        if (rc < 0) return rc;
+        uint64_t cur = c->ext_bound.load(std::memory_order_relaxed);
+        if (nb < cur) c->ext_bound.store(nb, std::memory_order_release);
     }
     if (!sw.node_stop && __atomic_load_n(&n->stop, __ATOMIC_ACQUIRE) != 0u) {
         sw.node_stop = true;
@@ -344,6 +351,12 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         slot.counted = true;
         consumed = lj + 1;
         const Snap &sn = c->h_snap[seq % kRing];
+        // The watcher may have put the node slot's best into Ctrl::best before this thread
+        // saw it: read the slot now (its best only decreases) so ext_bound covers it.
+        if (c->node) {
+            const int prc = poll_node(c, sw);
+            if (prc < 0) return prc;
+        }
         if (sn.best < bound) {
             // Ctrl::best = min(this search's hits, bounds injected by dpow_search_bound
             // or from the node slot).  At or above the lowest injected bound it is not a
@@ -405,6 +418,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), &worker_blocks);
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
+        L.poll_wb = c->poll_override ? c->poll_override : launch_poll_wb(ntz, L.rbits);
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
         L.done_target = done_target;
         L.ctrl = c->d_ctrl;
@@ -412,6 +426,8 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         L.stale = c->d_cancel + kStaleWord;
         L.snap = c->d_snap + seq % kRing;
         L.seq = (uint32_t)(seq + 1);
+        L.node_best = c->d_node ? reinterpret_cast<const unsigned long long *>(&c->d_node->best) : nullptr;
+        L.node_stop = c->d_node ? &c->d_node->stop : nullptr;
         e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L, (uint32_t)(worker_blocks + 1),
                           c->stream, slot.start, slot.end);
         if (e != hipSuccess) return hip_fail(e, "search_launch");
@@ -477,6 +493,7 @@ int dpow_open(int device, dpow_ctx **out) {
         return hip_fail(e, "hipGetDeviceProperties");
     }
     c->cus = (uint32_t)prop.multiProcessorCount;
+    if (const char *pw = getenv("DPOW_DIAG_POLL_WB")) c->poll_override = (uint32_t)std::max(0, atoi(pw));
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->bound_stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->reset_ev, hipEventDisableTiming)) != hipSuccess ||
@@ -520,6 +537,7 @@ void dpow_close(dpow_ctx *c) {
         (void)hipStreamDestroy(c->bound_stream);
     }
     if (c->reset_ev) (void)hipEventDestroy(c->reset_ev);
+    for (void *p : c->registered) (void)hipHostUnregister(p);
     delete c;
 }
 
@@ -557,7 +575,26 @@ int dpow_search_bound(dpow_ctx *c, uint64_t global_idx) {
 
 int dpow_node_attach(dpow_ctx *c, dpow_node_slot *slot) {
     if (!c) return set_error(DPOW_EINVAL, "dpow_node_attach: ctx is NULL");
+    if (!slot) {
+        c->node = c->d_node = nullptr;
+        return 0;
+    }
+    if (((uintptr_t)slot & 7u) != 0u) return set_error(DPOW_EINVAL, "dpow_node_attach: slot not 8-byte aligned");
+    // Map the slot's host page(s) for the watcher (fine-grained: hipHostRegister's
+    // default), once per page per context; unregistered at dpow_close.
+    DPOW_HIP(hipSetDevice(c->device));
+    const uintptr_t pg = 4096;
+    for (uintptr_t a = (uintptr_t)slot & ~(pg - 1); a < (uintptr_t)slot + sizeof(dpow_node_slot); a += pg) {
+        void *p = (void *)a;
+        if (std::find(c->registered.begin(), c->registered.end(), p) != c->registered.end()) continue;
+        const hipError_t e = hipHostRegister(p, pg, hipHostRegisterMapped);
+        if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) return hip_fail(e, "dpow_node_attach: hipHostRegister");
+        if (e == hipSuccess) c->registered.push_back(p);
+    }
+    void *d = nullptr;
+    DPOW_HIP(hipHostGetDevicePointer(&d, slot, 0));
     c->node = slot;
+    c->d_node = (dpow_node_slot *)d;
     return 0;
 }
 

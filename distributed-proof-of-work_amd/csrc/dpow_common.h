@@ -112,6 +112,8 @@ struct Launch {
     uint64_t n_big;        // claims of `chunk` wave-blocks
     uint64_t n_chunks;     // claims covering n_wblocks (n_big + tail claims)
     uint64_t n_head;       // the claims every wave takes at its start (2 per wave): hashed at raised priority
+    uint32_t poll_wb;      // wave-blocks per group: a wave reads Ctrl::best / Ctrl::stop once per group
+    uint32_t pad0;
     unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;
@@ -119,6 +121,12 @@ struct Launch {
     const uint32_t *stale;   // pinned: launches with seq <= *stale (mod 2^32) belong to a cancelled search
     Snap *snap;              // device alias of this launch's pinned completion record
     uint32_t seq;            // value the last workgroup writes to snap->seq
+    uint32_t pad1;
+    // Node slot (dpow_node_attach; null when none): device aliases of the slot's best and
+    // stop in the node's shared host memory, polled by the watcher -- another rank's hit
+    // lowers Ctrl::best, a raised stop stops the launch.
+    const unsigned long long *node_best;
+    const uint32_t *node_stop;
 };
 
 // Nibble positions (bit offsets) of a digest word in hex-string order from the

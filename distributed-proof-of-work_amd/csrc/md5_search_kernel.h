@@ -57,9 +57,10 @@ namespace dpow {
 #ifndef DPOW_SGPR_LONG_W0
 #define DPOW_SGPR_LONG_W0 8
 #endif
-// A wave polls Ctrl::best / Ctrl::stop every DPOW_POLL_WB wave-blocks of a
-// chunk (0: once per chunk).  profiles/r01_ab_poll.log: 0 / 12 / 16 / 32 ->
-// 216.3 / 217.8 / 218.3 / 218.6 GH/s, time-to-secret N=7 1.57 / 1.47 / 1.49 / 1.56 ms.
+// A wave polls Ctrl::best / Ctrl::stop once per group of Launch::poll_wb wave-blocks
+// of a chunk (the host's choice: plan.h launch_poll_wb); DPOW_POLL_WB = 0 builds the
+// once-per-chunk loop instead (A/B switch).  profiles/r01_ab_poll.log: 0 / 12 / 16 / 32
+// -> 216.3 / 217.8 / 218.3 / 218.6 GH/s, time-to-secret N=7 1.57 / 1.47 / 1.49 / 1.56 ms.
 #ifndef DPOW_POLL_WB
 #define DPOW_POLL_WB 16
 #endif
@@ -83,7 +84,6 @@ namespace dpow {
 #define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch;
                             // one final block only, search_body kDeferClaims)
 #endif
-constexpr uint32_t kPollWb = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 1;
 // Diagnostic builds only (tools/wave_trace.py): every worker wave records
 // {start, first claim, exit} in s_memrealtime ticks (100 MHz) and its hashed
 // wave-blocks, read back with dpow_diag_wave_trace.
@@ -618,14 +618,31 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 // was still queued when its search returned CANCELLED stops too, even after
 // the caller cleared the flag for its next task: the host marks every launch
 // up to the last one it queued as stale (int32 sequence distance).
+//
+// With a node slot attached (Launch::node_best / node_stop: the node's shared host
+// memory, mapped), it relays the node's Found fan-out the same way: a lower best of
+// another rank goes to Ctrl::best (atomicMin) -- the waves stop at it at their next
+// group -- and a raised node stop stops the launch.  The host injecting the same best
+// through a kernel on a second stream took 50-160 us to start that kernel beside the
+// running grid (profiles/r03_stop_latency.json).
 DPOW_DEV void watcher(const Launch &L) {
     if (threadIdx.x != 0) return;
+    unsigned long long node_seen = ~0ull;
     for (;;) {
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (done >= L.done_target) return;
         const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (__hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
-            (int32_t)(stale - L.seq) >= 0) {
+        bool stop = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+                    (int32_t)(stale - L.seq) >= 0;
+        if (L.node_best) {
+            const unsigned long long nb = __hip_atomic_load(L.node_best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (nb < node_seen) {
+                node_seen = nb;
+                __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            stop = stop || __hip_atomic_load(L.node_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+        }
+        if (stop) {
             __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
@@ -858,7 +875,7 @@ DPOW_DEV void search_body(const Launch &L) {
             global_of_local(i_first < L.i_begin ? L.i_begin : i_first, L.rbits, L.base_tb) >= best)
             break;
 #if DPOW_POLL_WB > 0
-        // The chunk runs in groups of kPollWb wave-blocks.  Each group's loads of
+        // The chunk runs in groups of L.poll_wb wave-blocks.  Each group's loads of
         // Ctrl::best / Ctrl::stop are issued before it and consumed after it (the
         // latency hides behind the hashing), so a hit elsewhere or a cancel ends
         // this wave within one group, not at the chunk's end.  A hit of this wave
@@ -866,8 +883,9 @@ DPOW_DEV void search_body(const Launch &L) {
         // Down-counters keep the loop's live SGPRs at a plain loop's count.
         uint64_t i0 = i_first;
         uint32_t left = nb;
+        const uint32_t poll_wb = L.poll_wb;
         for (;;) {
-            uint32_t q = left < kPollWb ? left : kPollWb;
+            uint32_t q = left < poll_wb ? left : poll_wb;
 #if DPOW_SPAN
             // A chunk never straddles a 2^24-k segment boundary (the host aligns a
             // spanning launch's chunks to them, dpow_api.cpp), so neither does a

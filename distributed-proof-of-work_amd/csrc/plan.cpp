@@ -216,6 +216,11 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
     return 0;
 }
 
+uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits) {
+    const uint32_t slow = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 16;
+    return expected_first_hit(ntz, rbits) <= kFastPollCands ? kFastPollWb : slow;
+}
+
 uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits) {
 #if DPOW_SMALL_GRIDS
     // Candidates of this partition expected before its first hit: 16^N R / 256.

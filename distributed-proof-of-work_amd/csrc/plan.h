@@ -75,6 +75,22 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
 // Mean number of a partition's candidates before its first hit at N trailing zeros.
 uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits);
 
+// Wave-blocks per poll group (Launch::poll_wb).  A wave reads Ctrl::best / Ctrl::stop
+// once per group, issued before the group and consumed after it, so a hit elsewhere,
+// an injected bound (the node board) or a cancel reaches it within two groups.  Long
+// groups cost less issue (DPOW_POLL_WB = 16 for searches expected to run for more than
+// kFastPollCands candidates -- the sweep, N >= 9), short ones (kFastPollWb) shorten the
+// drain after a hit when the whole search is expected to be short.
+#ifndef DPOW_POLL_WB
+#define DPOW_POLL_WB 16  // (also md5_search_kernel.h)
+#endif
+#ifndef DPOW_FAST_POLL_WB
+#define DPOW_FAST_POLL_WB 4
+#endif
+constexpr uint32_t kFastPollWb = DPOW_FAST_POLL_WB;
+constexpr uint64_t kFastPollCands = 1ull << 30;
+uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
+
 // Worker workgroups per CU for one launch (before the device share).  The full
 // persistent grid (kMaxBlocksPerCu = 6) has the highest rate, but a launch that is
 // short -- few candidates, or a first hit expected early (16^N candidates of the

@@ -12,7 +12,8 @@ hit, or a non-owner's time to notice the posted hit and drain.  This runs
 
   1. the owner alone (world = G, no process group): t_owner;
   2. every other rank alone, with a thread that posts the owner's hit to the board
-     slot t_owner after the rank's search started (as the owner's process would);
+     slot when the owner's search posted it (its dpow_search returning FOUND, measured
+     in step 1), counted from the rank's own start, as the owner's process would;
 
 and reports max over ranks, next to one GPU's Miner.mine (G1) and the world-1 RCCL
 batch boundary (pinned copy + all-reduce + copy + synchronize), which the real node
@@ -64,6 +65,14 @@ def main():
                 assert r.global_idx == exp[(tuple(nonce), n)]
             out["g1_ms"][f"{bytes(nonce).hex()}/{n}"] = med(ts)
 
+        found_at = {}
+
+        def search_timed(*a):
+            r = search(*a)
+            if r.status == distpow.FOUND:
+                found_at["t"] = time.perf_counter()  # dpow_search posted its hit just before returning
+            return r
+
         def run_rank(nonce, n, rank, G, post_after_s=None, g=None):
             slot = board.begin()
             stop = threading.Event()
@@ -83,23 +92,27 @@ def main():
             if post_after_s is not None:
                 th = threading.Thread(target=poster, args=(t0,))
                 th.start()
-            res = node_mine(search, nonce, n, rank, G, device=dev, board=board, attach_fn=m.attach_node)
+            found_at.clear()
+            res = node_mine(search_timed, nonce, n, rank, G, device=dev, board=board, attach_fn=m.attach_node)
             dt = time.perf_counter() - t0
+            t_post = found_at.get("t", t0 + dt) - t0
             stop.set()
             if th:
                 th.join()
-            return res, dt
+            return res, dt, t_post
 
         for G in (2, 4, 8):
             for nonce, n in want:
                 g = exp[(tuple(nonce), n)]
                 o = owner_rank(g, G)
-                t_own = []
+                t_own, t_posts = [], []
                 for _ in range(runs):
-                    res, dt = run_rank(nonce, n, o, G)
+                    res, dt, tp = run_rank(nonce, n, o, G)
                     assert res.status == distpow.FOUND and res.global_idx == g, (nonce, n, G, res)
                     t_own.append(dt)
+                    t_posts.append(tp)
                 t_o = sorted(t_own)[len(t_own) // 2]
+                t_p = sorted(t_posts)[len(t_posts) // 2]  # when the owner's search posted its hit
                 per_rank = []
                 for r in range(G):
                     if r == o:
@@ -107,7 +120,7 @@ def main():
                         continue
                     ts = []
                     for _ in range(runs):
-                        res, dt = run_rank(nonce, n, r, G, post_after_s=t_o, g=g)
+                        res, dt, _ = run_rank(nonce, n, r, G, post_after_s=t_p, g=g)
                         # bounded by the posted hit (EXHAUSTED of this rank's batch -> no
                         # process group: node_mine reports the rank's own status), never a
                         # hit above it

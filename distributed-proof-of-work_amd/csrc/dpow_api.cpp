@@ -175,6 +175,7 @@ struct dpow_ctx {
     std::atomic<uint64_t> ext_bound{DPOW_NO_HIT};  // the lowest bound injected into the running search
     hipStream_t bound_stream = nullptr;
     hipEvent_t reset_ev = nullptr;
+    hipEvent_t reset_done = nullptr;  // the running search's start kernel is done (reset_ev, or its timing event)
     // Node slot (dpow_node_attach): shared by the ranks of one node, polled while a
     // search waits for its records.
     dpow_node_slot *node = nullptr;
@@ -213,7 +214,7 @@ int inject_bound_locked(dpow_ctx *c, uint64_t g) {
     if (g >= c->ext_bound.load(std::memory_order_relaxed)) return 0;
     c->ext_bound.store(g, std::memory_order_release);
     DPOW_HIP(hipSetDevice(c->device));
-    DPOW_HIP(hipStreamWaitEvent(c->bound_stream, c->reset_ev, 0));  // after this search's reset
+    DPOW_HIP(hipStreamWaitEvent(c->bound_stream, c->reset_done, 0));  // after this search's reset
     const hipError_t e = search_bound(c->d_ctrl, g, c->bound_stream);
     if (e != hipSuccess) return hip_fail(e, "search_bound");
     return 0;
@@ -302,9 +303,44 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     // (as an injected bound: a record at or above it is not a hit of ours).
     const uint64_t node_best = c->node ? __atomic_load_n(&c->node->best, __ATOMIC_ACQUIRE) : DPOW_NO_HIT;
     sw.node_seen = node_best;
-    hipError_t e = search_reset(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot),
-                                node_best < bound ? node_best : bound, c->stream, c->reset_ev);
-    if (e != hipSuccess) return hip_fail(e, "search_reset");
+    const uint64_t seq0 = c->seq;
+    size_t launched = 0, consumed = 0;
+    int64_t busy_until = 0;  // expected end of the launches queued so far (now_ns clock)
+    PlannedLaunch pl;
+    bool have = planner.next(pl);
+    // The start kernel resets the control block and claim counters; when the window holds
+    // k = 0 it also hashes those R candidates (search_ctrl.hip) and counts as launch 0 of
+    // the search, with a completion record of its own.
+    StartK0 k0{};
+    LaunchSlot *k0slot = nullptr;
+    if (have && pl.k0) {
+        k0slot = &c->slots[seq0 % kRing];
+        if (harvest(c, *k0slot) < 0) return DPOW_EHIP;
+        k0.r = (uint32_t)(pl.L.i_end - pl.L.i_begin);
+        k0.base_tb = pl.L.base_tb;
+        k0.nblk = pl.info.nblk;
+        k0.p = 4 * pl.info.w0 + pl.info.sh;
+        k0.ntz = ntz;
+        k0.seq = (uint32_t)(seq0 + 1);
+        k0.snap = c->d_snap + seq0 % kRing;
+        memcpy(k0.iv, pl.L.iv, sizeof k0.iv);
+        memcpy(k0.T, pl.L.T, sizeof k0.T);
+    }
+    c->reset_done = k0slot ? k0slot->end : c->reset_ev;
+    hipError_t e = search_start(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot),
+                                node_best < bound ? node_best : bound, k0, c->stream,
+                                k0slot ? k0slot->start : nullptr, c->reset_done);
+    if (e != hipSuccess) return hip_fail(e, "search_start");
+    if (k0slot) {
+        k0slot->pending = true;
+        k0slot->counted = false;
+        k0slot->candidates = k0.r;
+        k0slot->g_end = 1ull << 8;
+        c->seq = seq0 + 1;
+        launched = 1;
+        busy_until = now_ns() + kEstFixedNs;
+        have = planner.next(pl);
+    }
     // Open the window for dpow_search_bound; closed (and its atomicMin kernels
     // drained, so none lands on the next search's reset) on every return path.
     struct BoundWindow {
@@ -323,9 +359,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         }
     } bound_window(c, node_best);
 
-    const uint64_t seq0 = c->seq;
     uint32_t done_target = 0;
-    size_t launched = 0, consumed = 0;
     // Launches still queued when the search returns -- behind a hit, a bound, a
     // cancel or an error -- are marked stale, so their watchers stop them at once
     // even if the caller clears the cancel flag for its next task before they
@@ -374,9 +408,6 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
             return DPOW_CANCELLED;
         return DPOW_EXHAUSTED;
     };
-    int64_t busy_until = 0;  // expected end of the launches queued so far (now_ns clock)
-    PlannedLaunch pl;
-    bool have = planner.next(pl);
     while (status == DPOW_EXHAUSTED && have) {
         if (sw.node_stop) {
             status = DPOW_CANCELLED;

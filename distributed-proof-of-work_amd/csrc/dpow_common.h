@@ -54,6 +54,13 @@ constexpr uint32_t kBop3I = 0x39;  // I = y ^ (x | ~z)
 #define DPOW_SPAN 1
 #endif
 
+// Launches span chunk lengths 1..3 for SH = 0 layouts (plan.cpp lspan_layout; the kernel
+// re-derives the pad and bit-length words per chunk length).  A/B switch: 0 = one launch
+// per chunk length, as in round 2.
+#ifndef DPOW_LSPAN
+#define DPOW_LSPAN 1
+#endif
+
 // Candidates per lane per wave-block (interleaved for ILP).
 #ifndef DPOW_NC
 #define DPOW_NC 2
@@ -127,7 +134,39 @@ struct Launch {
     // lowers Ctrl::best, a raised stop stops the launch.
     const unsigned long long *node_best;
     const uint32_t *node_stop;
+    // SH = 0 layouts below k = 2^24: T / KT hold the message of chunk length 0 (the pad at
+    // byte 1 of word W0, bit length 8 (nonce_len + 1)) with the launch's block count, and a
+    // candidate of chunk length l adds lseg_deltas(l) to words W0, W0 + 1 and the bit-length
+    // word.  The kernel treats the chunk lengths as segments (seg_id): a wave re-derives those
+    // words' K + M when it enters another one, so one launch may span chunk lengths 1..3
+    // (lspan: host-side planning information only).
+    uint32_t lspan;
+    uint32_t seg0;         // segment id of the template (the kernel's first segment)
 };
+
+// Chunk length of k < 2^24 (nextChunk^k, worker.go:234-244): 0 for k = 0, else 1 + floor(log256 k).
+DPOW_HD uint32_t chunk_len_lt24(uint32_t k) { return (k != 0u) + (k > 0xFFu) + (k > 0xFFFFu); }
+
+// Additions of chunk length l (0..3) to words W0, W0 + 1 and the bit-length word of an
+// SH = 0 layout against chunk length 0 (Launch: the template of an SH = 0 launch below
+// k = 2^24): the 0x80 pad moves from byte 1 of W0 to byte 1 + l of the (W0, W0 + 1) pair,
+// and the bit length grows by 8 l.  Shared by the kernel and the planner.
+DPOW_HD void lseg_deltas(uint32_t l, uint32_t &d0, uint32_t &d1, uint32_t &dlen) {
+    const uint64_t pad = 0x80ull << (8 * (1 + l));
+    d0 = (uint32_t)pad - 0x8000u;
+    d1 = (uint32_t)(pad >> 32);
+    dlen = 8u * l;
+}
+
+// Segment id of chunk k: a launch is uniform within a segment except for the variable
+// bytes.  k >> 24 for k >= 2^24 (2^24-k segments, spanned by launches at L >= 4); kLsegBase + L
+// below (chunk lengths 0..3, spanned by Launch::lspan launches).
+// (The id needs no Launch field: reading Launch::lspan in the kernel's group loop moved its
+// wave-uniform index arithmetic onto the VALU, +10 VALU per wave-block, tools/isa_loop.py.)
+constexpr uint32_t kLsegBase = 0xFFFFFFF0u;  // ids of chunk lengths 0..3 (k >> 24 < 2^31 below DPOW_K_LIMIT)
+DPOW_HD uint32_t seg_id(uint64_t k) {
+    return k >> 24 ? (uint32_t)(k >> 24) : kLsegBase + chunk_len_lt24((uint32_t)k);
+}
 
 // Nibble positions (bit offsets) of a digest word in hex-string order from the
 // end: the last hex character is the low nibble of the word's top byte.

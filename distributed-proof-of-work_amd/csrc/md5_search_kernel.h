@@ -138,9 +138,12 @@ struct KConst {
 // wave-uniform per wave-block anyway (VarWords::hi_s, which carries the
 // segment addition too), so only SH = 0's W0 + 1 and SH = 3's W0 + 2 are
 // VGPR-held segment words.
+// SH = 0 kernels also serve launches spanning chunk-length segments (Launch::lspan):
+// there the bit-length word (16 NBLK - 2) and W0 + 1 (the pad of L = 3) change per segment.
 template <int NBLK, int W0, int SH>
 DPOW_DEV_CONST bool seg_word(int m) {
-    return DPOW_SPAN && ((SH == 0 && m == W0 + 1) || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2));
+    return (DPOW_SPAN && ((SH == 0 && m == W0 + 1) || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2))) ||
+           (DPOW_LSPAN && SH == 0 && (m == W0 + 1 || m == 16 * NBLK - 2));
 }
 
 // First hand-ordered step of block 0: W0 + pipe_lead<NBLK, W0, SH>.  4 is the first
@@ -253,18 +256,46 @@ DPOW_DEV void seg_deltas(const Launch &L, uint32_t seg, uint32_t &d1, uint32_t &
     seg_word_deltas(L.T[W0 + 1], L.T[W0 + 2], seg, L.seg_first, SH, d1, d2);
 }
 
+// Addition to segment word m: d[0] to W0 + 1, d[1] to W0 + 2, d[2] to the bit-length word
+// (where W0 + 1 is the bit-length word, plan.cpp puts the whole difference in d[2]).
+template <int NBLK, int W0>
+DPOW_DEV uint32_t seg_add(int m, const uint32_t (&d)[3]) {
+    return m == 16 * NBLK - 2 ? d[2] : m == W0 + 1 ? d[0] : d[1];
+}
+
+// The segment-word additions of segment sg (seg_id): for SH = 0 below k = 2^24 the
+// chunk-length deltas against the template's chunk length 0 (lseg_deltas: no Launch field is
+// read -- plain kernarg reads here were hoisted out of the claim loop into SGPRs and pushed
+// its wave-uniform index arithmetic onto the VALU, +10 VALU per wave-block in <1,1,0>,
+// tools/isa_loop.py), else the 2^24-k field (seg_word_deltas); d0 = the addition to W0.
+template <int NBLK, int W0, int SH>
+DPOW_DEV void seg_all_deltas(const Launch &L, uint32_t sg, uint32_t &d0, uint32_t (&d)[3]) {
+    d0 = d[0] = d[1] = d[2] = 0u;
+    if (sg >= kLsegBase) {
+        if constexpr (SH == 0 && DPOW_LSPAN) {
+            lseg_deltas((sg - kLsegBase) & 3u, d0, d[0], d[2]);
+            if constexpr (W0 + 1 == 16 * NBLK - 2) {  // W0 + 1 is the bit-length word
+                d[2] += d[0];
+                d[0] = 0u;
+            }
+        }
+    } else {
+        seg_deltas<W0, SH>(L, sg, d[0], d[1]);
+    }
+}
+
 // Re-derive the VGPR-held K + M constants of the segment words (wave-uniform,
 // once per segment change: a rare branch).
 template <int NBLK, int W0, int SH, int BLK, int I>
-DPOW_DEV void kconst_seg(KConst &kc, const Launch &L, uint32_t d1, uint32_t d2) {
+DPOW_DEV void kconst_seg(KConst &kc, const Launch &L, const uint32_t (&d)[3]) {
     if constexpr (BLK < NBLK) {
         if constexpr (VgprK<NBLK, W0, SH>::seg(BLK, I)) {
             constexpr int m = 16 * BLK + md5_word(I);
-            const uint32_t k = L.KT[64 * BLK + I] + (m == W0 + 1 ? d1 : d2);
+            const uint32_t k = L.KT[64 * BLK + I] + seg_add<NBLK, W0>(m, d);
             asm volatile("v_mov_b32 %0, %1" : "=v"(kc.v[64 * BLK + I]) : "s"(k));
         }
-        if constexpr (I + 1 < 64) kconst_seg<NBLK, W0, SH, BLK, I + 1>(kc, L, d1, d2);
-        else kconst_seg<NBLK, W0, SH, BLK + 1, 0>(kc, L, d1, d2);
+        if constexpr (I + 1 < 64) kconst_seg<NBLK, W0, SH, BLK, I + 1>(kc, L, d);
+        else kconst_seg<NBLK, W0, SH, BLK + 1, 0>(kc, L, d);
     }
 }
 
@@ -277,8 +308,9 @@ struct VarWords {
                          //  segment addition d1
     uint32_t lane_k;     // SH = 3: the per-lane part of V >> 8 (the lane's k offset; 0 when R >= 64)
     const KConst *kc;    // launch-uniform K + M constants held in VGPRs (segment words: current segment)
-    uint32_t seg_d[2];   // segment-word additions for the steps that read them from L.KT (full_check's
-                         //  steps 62-63 of the last block only; the hash loop holds them all in kc)
+    uint32_t seg_d[3];   // segment-word additions (seg_add) for the steps that read them from L.KT
+                         //  (full_check's steps 62-63 of the last block only; the hash loop holds them
+                         //  all in kc)
 };
 
 // K + M of step I of block BLK for candidate j (the message word M includes the
@@ -295,7 +327,7 @@ struct StepWord {
     static constexpr bool seg = seg_word<NBLK, W0, SH>(m);
     static DPOW_DEV uint32_t km(const Launch &L, const VarWords &v, int j) {
         uint32_t k = zero_word ? kMd5K[I] : vgpr_k ? v.kc->v[64 * BLK + I] : L.KT[64 * BLK + I];
-        if constexpr (seg && !vgpr_k) k += v.seg_d[m == W0 + 1 ? 0 : 1];
+        if constexpr (seg && !vgpr_k) k += seg_add<NBLK, W0>(m, v.seg_d);
         if constexpr (m == W0) k = (k + v.lo_s[j]) + v.lo_v;
         if constexpr (SH != 0 && m == W0 + 1) {
             k += v.hi_s[j];                        // SALU: K + M stays uniform
@@ -586,11 +618,17 @@ DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff, uint32_t
 
 // Full digest test of one lane's candidate (rare path: only when the D-word
 // test passed and ntz > 8, i.e. probability 2^-32 per candidate).
+// loff: the lane offset, plus (SH = 0) the segment's addition to word W0 (search_body lov);
+// sd: the segment's word additions (seg_all_deltas), computed by the caller outside the
+// per-lane branch (a dynamic kernarg index inside it moved the hash loop's wave-uniform
+// index arithmetic onto the VALU: +10 VALU per wave-block in <1,1,0>, tools/isa_loop.py).
 template <int NBLK, int W0, int SH>
-DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_t loff, uint64_t i0) {
+DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_t loff, const uint32_t (&sd)[3]) {
     VarWords v;
     v.kc = &kc;
-    seg_deltas<W0, SH>(L, (uint32_t)((i0 >> L.rbits) >> 24), v.seg_d[0], v.seg_d[1]);
+    v.seg_d[0] = sd[0];
+    v.seg_d[1] = sd[1];
+    v.seg_d[2] = sd[2];
     var_words<SH>(v, 0, vs, loff, v.seg_d[0]);
     uint32_t out[4][kNC];
     md5_tail<NBLK, W0, SH, 1>(out, L, v);
@@ -705,7 +743,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
     uint32_t vs[kNC];
     VarWords v;
     v.kc = &kc;
-    v.seg_d[0] = v.seg_d[1] = 0u;  // unused: the hash loop's segment-word steps all read kc
+    v.seg_d[0] = v.seg_d[1] = v.seg_d[2] = 0u;  // unused: the hash loop's segment-word steps all read kc
     uint32_t d1 = 0u;               // SH != 0: the segment addition to word W0 + 1 (both slots share
     if constexpr (SH != 0) {        //  the segment: wave-blocks never straddle one)
         uint32_t d2;
@@ -733,7 +771,9 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
             uint64_t m = bal[j] & lane_range_mask((int64_t)(L.i_begin - ij), (int64_t)(L.i_end - ij));
             if (!EQ && m != 0) m &= __ballot((dig[3][j] & L.dmask) == 0u);
             if (m != 0 && L.ntz > 8u) {
-                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, kc, vs[j], loff, ij);
+                uint32_t d0, sd[3];
+                seg_all_deltas<NBLK, W0, SH>(L, seg_id(ij >> L.rbits), d0, sd);
+                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, kc, vs[j], loff, sd);
                 m = __ballot(ok);
             }
             if (m != 0) {
@@ -785,8 +825,12 @@ DPOW_DEV void search_body(const Launch &L) {
     // (wave-uniform, read once per group): an SGPR live across the hash loop
     // costs spill reloads inside it under the 80-SGPR budget.
     uint32_t cur_seg_v;
-    asm("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(L.seg_first));
+    asm("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(L.seg0));
 #endif
+    // SH = 0: the lane offset plus the current segment's addition to word W0 (the 0x80 pad
+    // of chunk lengths <= 2 in launches spanning chunk lengths; 0 in the template's own
+    // segment), the per-lane part of W0's K + M.
+    uint32_t lov = loff;
 
     unsigned long long best = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t stop = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -893,12 +937,13 @@ DPOW_DEV void search_body(const Launch &L) {
             // constants.  (Splitting groups at boundaries in the kernel instead
             // costs 4 SGPR spill reloads per wave-block: tools/isa_loop.py.)
             {
-                const uint32_t sg = (uint32_t)((i0 >> L.rbits) >> 24);
+                const uint32_t sg = seg_id(i0 >> L.rbits);
                 if (sg != __builtin_amdgcn_readfirstlane(cur_seg_v)) {
                     asm volatile("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(sg));
-                    uint32_t d1, d2;
-                    seg_deltas<W0, SH>(L, sg, d1, d2);
-                    kconst_seg<NBLK, W0, SH, 0, 0>(kc, L, d1, d2);
+                    uint32_t d0, d[3];
+                    seg_all_deltas<NBLK, W0, SH>(L, sg, d0, d);
+                    kconst_seg<NBLK, W0, SH, 0, 0>(kc, L, d);
+                    if constexpr (SH == 0) lov = lane_offset(L.rbits, lane) + d0;
                 }
             }
 #endif
@@ -911,7 +956,7 @@ DPOW_DEV void search_body(const Launch &L) {
 #if DPOW_WAVE_TRACE
                 ++n_wb;
 #endif
-                const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, kc, i0, lane, loff);
+                const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, kc, i0, lane, SH == 0 ? lov : loff);
                 if (g != kNoHitG) {
                     best = g < best ? g : best;
                     hit = true;

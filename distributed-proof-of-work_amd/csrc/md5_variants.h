@@ -39,8 +39,22 @@ hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu);
 hipError_t search_bound(Ctrl *ctrl, unsigned long long g, hipStream_t stream);
 
 // Per-search reset of the control block and claim counters (search_ctrl.hip).
-// done_ev (may be null) is recorded by the reset kernel's dispatch.
-hipError_t search_reset(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
-                        hipStream_t stream, hipEvent_t done_ev);
+// The search's start kernel (search_ctrl.hip): resets the control block to `bound` and the
+// claim counters, and -- when k0.r > 0 -- hashes the k = 0 candidates (msg = nonce ||
+// threadByte, R of them), their first hit to Ctrl::best, then writes k0.snap's record.
+struct StartK0 {
+    uint32_t r;        // threadBytes of the partition (R), 0 = no k = 0 work
+    uint32_t base_tb;  // uint8(worker_byte << R_bits)
+    uint32_t nblk;     // final blocks of the k = 0 message
+    uint32_t p;        // byte offset of the threadByte in them
+    uint32_t ntz;
+    uint32_t seq;      // record value (launch sequence + 1)
+    Snap *snap;        // completion record (device alias of the pinned slot)
+    uint32_t iv[4];    // chaining value entering the final blocks
+    uint32_t T[32];    // their words, threadByte zeroed (plan.cpp build_template)
+};
+// start / stop (may be null) are recorded by the kernel's own dispatch.
+hipError_t search_start(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
+                        const StartK0 &k0, hipStream_t stream, hipEvent_t start, hipEvent_t stop);
 
 }  // namespace dpow

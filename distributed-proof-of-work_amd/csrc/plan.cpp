@@ -72,20 +72,15 @@ int WindowPlanner::init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, ui
     return 0;
 }
 
-bool WindowPlanner::next(PlannedLaunch &pl) {
-    if (k_ >= k_end_) return false;
-    const uint64_t k = k_;
-    uint64_t ke = segment_end(k) < k_end_ ? segment_end(k) : k_end_;
-    if (const uint64_t w2 = word2_period(p_ % 4)) {  // word W0 + 2 changes: end the launch
-        const uint64_t we = (k / w2 + 1) * w2;
-        if (we < ke) ke = we;
-    }
-    const uint32_t L = chunk_len_of(k);
-    const size_t msg_len = nonce_len_ + 1 + L;
-    const size_t total_blocks = (msg_len + 8) / 64 + 1;
-    const uint32_t nblk = (uint32_t)(total_blocks - blk_v_);
-    memset(&pl, 0, sizeof pl);
-    Launch &Lh = pl.L;
+uint32_t WindowPlanner::nblk_of(uint32_t chunk_len) const {
+    const size_t msg_len = nonce_len_ + 1 + chunk_len;
+    return (uint32_t)((msg_len + 8) / 64 + 1 - blk_v_);
+}
+
+// Final-block words of the message nonce || threadByte || chunk_k with the variable bytes
+// (threadByte and chunk bytes 0..2) zeroed: nonce tail, chunk bytes 3.. of k, the 0x80 pad
+// and the bit length (RFC 1321 3.1-3.2).
+void WindowPlanner::build_template(uint64_t k, uint32_t L, uint32_t nblk, uint32_t T[32]) const {
     uint8_t buf[128];
     memset(buf, 0, sizeof buf);
     const uint32_t p = p_;
@@ -93,14 +88,71 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     // buf[p] = threadByte and buf[p+1 .. p+min(L,3)] = low chunk bytes: variable (left 0).
     for (uint32_t j = 3; j < L; ++j) buf[p + 1 + j] = (uint8_t)(k >> (8 * j));
     buf[p + 1 + L] = 0x80;
-    const uint64_t bits = (uint64_t)msg_len * 8u;
+    const uint64_t bits = (uint64_t)(nonce_len_ + 1 + L) * 8u;
     for (int j = 0; j < 8; ++j) buf[64 * nblk - 8 + j] = (uint8_t)(bits >> (8 * j));
+    for (uint32_t w = 0; w < 32; ++w) T[w] = w < 16 * nblk ? load_le32(buf + 4 * w) : 0u;
+}
+
+bool lspan_layout(size_t nonce_len, uint32_t rbits) {
+    // SH = 0: the pads of chunk lengths 0..3 fall in words W0 / W0 + 1, whose K + M the
+    // kernel re-derives per segment.  R >= 2: a power-of-two chunk of <= 2R wave-blocks puts
+    // the boundaries k = 256 and 65536 (256 R and 65536 R indices) on claim boundaries.
+    return DPOW_LSPAN && nonce_len % 4 == 0 && rbits >= 1;
+}
+
+bool WindowPlanner::lseg_template(uint64_t k) const {
+    return DPOW_LSPAN && p_ % 4 == 0 && k < (1ull << 24);
+}
+
+bool WindowPlanner::next(PlannedLaunch &pl) {
+    if (k_ >= k_end_) return false;
+    const uint64_t k = k_;
+    memset(&pl, 0, sizeof pl);
+    Launch &Lh = pl.L;
+    const uint32_t p = p_;
+    const uint64_t R = 1ull << rbits_;
+    uint64_t ke = segment_end(k) < k_end_ ? segment_end(k) : k_end_;
+    if (const uint64_t w2 = word2_period(p_ % 4)) {  // word W0 + 2 changes: end the launch
+        const uint64_t we = (k / w2 + 1) * w2;
+        if (we < ke) ke = we;
+    }
+    const uint32_t L = chunk_len_of(k);
+    const uint32_t nblk = nblk_of(L);
+    pl.k0 = DPOW_START_K0 && k == 0;
+    // (the start kernel hashes k = 0 from the real chunk-length-0 template: no deltas)
+    uint32_t L_last = L;
+    if (!pl.k0 && k >= 1 && k < (1ull << 24) && lspan_layout(nonce_len_, rbits_)) {
+        // Merge the following chunk lengths (up to 3) with the same block count.
+        uint64_t e = ke;
+        while (e < k_end_ && e < (1ull << 24) && nblk_of(chunk_len_of(e)) == nblk) {
+            e = segment_end(e) < k_end_ ? segment_end(e) : k_end_;
+            L_last = chunk_len_of(e - 1);
+        }
+        if (e > ke) {
+            ke = e;
+            Lh.lspan = 1;
+        }
+    }
+    build_template(k, L, nblk, Lh.T);
     for (int w = 0; w < 4; ++w) Lh.iv[w] = iv_[w];
-    for (uint32_t w = 0; w < 16 * nblk; ++w) Lh.T[w] = load_le32(buf + 4 * w);
+    if (lseg_template(k)) {
+        // SH = 0 below k = 2^24: the template of chunk length 0 with this block count (the
+        // kernel adds lseg_deltas(l) for a candidate of chunk length l, every segment).
+        uint32_t d0, d1, dlen;
+        lseg_deltas(L, d0, d1, dlen);
+        const uint32_t w0 = p / 4, lenw = 16 * nblk - 2;
+        if (w0 + 1 == lenw) {
+            dlen += d1;
+            d1 = 0;
+        }
+        Lh.T[w0] -= d0;
+        Lh.T[w0 + 1] -= d1;
+        Lh.T[lenw] -= dlen;
+    }
     for (uint32_t b = 0; b < nblk; ++b)
         for (int s = 0; s < 64; ++s) Lh.KT[64 * b + s] = kMd5K[s] + Lh.T[16 * b + md5_word(s)];
     Lh.i_begin = k << rbits_;
-    Lh.i_end = ke << rbits_;
+    Lh.i_end = pl.k0 ? R : ke << rbits_;
     Lh.wb_begin = Lh.i_begin & ~(uint64_t)(kWaveBlock - 1);
     Lh.n_wblocks = (Lh.i_end - Lh.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
     Lh.rbits = rbits_;
@@ -110,6 +162,8 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     Lh.deq = 0u - iv_[3];
     Lh.ntz = ntz_;
     Lh.seg_first = (uint32_t)(k >> 24);
+    Lh.seg0 = lseg_template(k) ? kLsegBase : seg_id(k);  // the template's own segment
+    if (pl.k0) ke = 1;
     pl.info.k_begin = k;
     pl.info.k_end = ke;
     pl.info.i_begin = Lh.i_begin;
@@ -118,6 +172,8 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     pl.info.w0 = p / 4;
     pl.info.sh = p % 4;
     pl.info.chunk_len = L;
+    pl.info.chunk_len_last = L_last;
+    pl.info.start_kernel = pl.k0 ? 1u : 0u;
     k_ = ke;
     return true;
 }
@@ -143,6 +199,18 @@ void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words
     const uint32_t sh = pl.info.sh, w0 = pl.info.w0;
     words[w0] += V << (8 * sh);
     if (sh) words[w0 + 1] += V >> (32 - 8 * sh);
+    if (Lh.seg0 == kLsegBase && !pl.k0) {  // SH = 0 below 2^24: md5_search_kernel.h seg_all_deltas
+        uint32_t d0, d1, dlen;
+        lseg_deltas(chunk_len_of(local_idx >> Lh.rbits), d0, d1, dlen);
+        const uint32_t lenw = 16 * pl.info.nblk - 2;
+        if (w0 + 1 == lenw) {
+            dlen += d1;
+            d1 = 0;
+        }
+        words[w0] += d0;
+        words[w0 + 1] += d1;
+        words[lenw] += dlen;
+    }
     if (DPOW_SPAN) {  // the segment words, as the kernel re-derives them (md5_search_kernel.h seg_word)
         uint32_t d1, d2;
         const uint32_t seg = (uint32_t)((local_idx >> Lh.rbits) >> 24);
@@ -177,12 +245,15 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
     uint64_t chunk = span_wb / (worker_blocks * wpb * kClaimsPerWave);
     if (chunk < kMinChunk) chunk = kMinChunk;
     if (chunk > kMaxChunk) chunk = kMaxChunk;
-    if (DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) {
+    if ((DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) || L.lspan) {
         // The launch spans 2^24-k segments: a power-of-two chunk and wave-blocks
         // counted from a multiple of chunk wave-blocks put every segment boundary
         // (a multiple of 2^24 * R indices) on a claim boundary, big or tail, so no
         // claim straddles one (the kernel switches constants per chunk group).
+        // Chunk-length segments (lspan) end at k = 256 and 65536, i.e. 2R and 512R
+        // wave-blocks: chunks of at most 2R wave-blocks.
         while (chunk & (chunk - 1)) chunk &= chunk - 1;
+        if (L.lspan && chunk > (2ull << L.rbits)) chunk = 2ull << L.rbits;
         L.wb_begin = L.i_begin & ~(chunk * (uint64_t)kWaveBlock - 1);
         L.n_wblocks = (L.i_end - L.wb_begin + (uint64_t)kWaveBlock - 1) / (uint64_t)kWaveBlock;
         // The realignment adds up to chunk - 1 wave-blocks: size the grid on the new count.

@@ -13,6 +13,9 @@ namespace dpow {
 struct PlannedLaunch {
     dpow_plan_launch info;
     Launch L;  // ctrl / cancel / claim / chunk / done_target filled at launch time
+    // k = 0 (the chunk of zero bytes, msg = nonce || threadByte): hashed by the search's
+    // start kernel (search_ctrl.hip), not by an md5 launch; L.iv / L.T hold its message.
+    bool k0 = false;
 };
 
 uint32_t chunk_len_of(uint64_t k);
@@ -20,6 +23,12 @@ uint64_t segment_end(uint64_t k);
 // k-period of word W0 + 2's chunk bytes for byte shift SH (0: launch-uniform
 // or a kernel segment word); the planner ends launches on its multiples.
 uint64_t word2_period(uint32_t sh);
+// The planner may merge chunk lengths 1..3 (k in [1, 2^24)) into one launch: SH = 0
+// layouts, R >= 2, equal block counts (WindowPlanner::next).
+bool lspan_layout(size_t nonce_len, uint32_t rbits);
+#ifndef DPOW_START_K0
+#define DPOW_START_K0 1  // k = 0 hashed by the search's start kernel (A/B switch)
+#endif
 uint32_t remainder_bits(uint32_t worker_bits);
 uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits);
 
@@ -32,6 +41,9 @@ class WindowPlanner {
     bool next(PlannedLaunch &out);  // false when the window is covered
 
    private:
+    uint32_t nblk_of(uint32_t chunk_len) const;
+    bool lseg_template(uint64_t k) const;  // the launch's template is chunk length 0's (SH = 0, k < 2^24)
+    void build_template(uint64_t k, uint32_t chunk_len, uint32_t nblk, uint32_t T[32]) const;
     const uint8_t *nonce_ = nullptr;
     size_t nonce_len_ = 0, blk_v_ = 0;
     uint32_t p_ = 0, ntz_ = 0, rbits_ = 0, base_tb_ = 0;

@@ -39,7 +39,8 @@ class PlanLaunch(ctypes.Structure):
     _fields_ = [("k_begin", ctypes.c_uint64), ("k_end", ctypes.c_uint64),
                 ("i_begin", ctypes.c_uint64), ("i_end", ctypes.c_uint64),
                 ("nblk", ctypes.c_uint32), ("w0", ctypes.c_uint32), ("sh", ctypes.c_uint32),
-                ("chunk_len", ctypes.c_uint32)]
+                ("chunk_len", ctypes.c_uint32), ("chunk_len_last", ctypes.c_uint32),
+                ("start_kernel", ctypes.c_uint32)]
 
 
 DPOW_MAX_NONCE = 1024

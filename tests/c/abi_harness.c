@@ -57,7 +57,10 @@ int main(int argc, char **argv) {
     if (dpow_trailing_zero_nibbles(d) != 0) return fail("dpow_trailing_zero_nibbles");
     dpow_plan_launch plan[8];
     const int n = dpow_plan_window(nonce, sizeof nonce, 0, 0, 0, (1u << 24) + 5, plan, 8);
-    if (n != 5 || plan[4].chunk_len != 4) return fail("dpow_plan_window");
+    /* k = 0 (start kernel), k in [1, 2^24) (chunk lengths 1..3 in one launch), then L = 4 */
+    if (n != 3 || !plan[0].start_kernel || plan[1].chunk_len != 1 || plan[1].chunk_len_last != 3 ||
+        plan[2].chunk_len != 4)
+        return fail("dpow_plan_window");
     if (dpow_abi_version() != DPOW_ABI_VERSION) return fail("dpow_abi_version");
     /* the node slot (host memory shared by a node's ranks): reset, post = atomic min, stop */
     dpow_node_slot slot;

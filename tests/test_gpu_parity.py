@@ -51,6 +51,42 @@ def test_nonce_lengths_golden(miner, golden):
             (len(e["nonce"]), e["ntz"], r)
 
 
+def test_chunk_length_spanning_launch_vs_oracle(miner, oracle):
+    """One md5 launch spans chunk lengths 1..3 (SH = 0 layouts, R >= 2: plan.cpp; the kernel
+    re-derives the pad and bit-length words per chunk length) after the start kernel has
+    hashed k = 0.  Walk each window's hits one by one -- every search starts right after
+    the previous hit's k, so launches start on both sides of k = 1, 256 and 65536 -- and
+    compare every first hit with the oracle."""
+    K_END = 70000
+    cases = [([1, 2, 3, 4], 5, 3, 3), ([1, 2, 3, 4], 7, 2, 3), ([], 6, 2, 3), (list(range(8)), 2, 4, 3),
+             (list(range(48)), 1, 5, 3), ([7] * 52, 3, 3, 3), (list(range(60)), 9, 5, 3), ([9] * 64, 0, 6, 2),
+             ([5, 6, 7, 8], 0, 2, 4)]
+    for nonce, wb, wbits, ntz in cases:
+        rb = 8 - wbits % 9
+        plan = distpow.plan_window(nonce, wb, wbits, 0, K_END)
+        assert plan[0].start_kernel == 1 and plan[1].k_begin == 1 and plan[1].chunk_len == 1
+        assert plan[1].chunk_len_last == (2 if len(nonce) == 52 else 3), (len(nonce), [(p.k_begin, p.k_end) for p in plan])
+        k, hits = 0, 0
+        while k < K_END and hits < 12:
+            exp = oracle.mine_window(nonce, ntz, wb, wbits, k, K_END)
+            r = miner.search(nonce, ntz, wb, wbits, k, K_END)
+            if exp is None:
+                assert r.status == EXHAUSTED, (len(nonce), wb, wbits, k, r)
+                break
+            assert r.status == FOUND and r.global_idx == exp[1] and list(r.secret) == list(exp[0]), \
+                (len(nonce), wb, wbits, k, r, exp)
+            hits += 1
+            k = (r.global_idx >> 8) + 1
+        assert hits >= 3, (len(nonce), wb, wbits)
+    # R = 256, hits across k = 65536 (the L = 2 -> 3 boundary inside the launch)
+    for nonce in ([1, 2, 3, 4], [2, 2, 2, 2]):
+        for k0 in (65530, 65000, 60000):
+            exp = oracle.mine_window(nonce, 4, 0, 0, k0, 66000)
+            r = miner.search(nonce, 4, 0, 0, k0, 66000)
+            assert (r.status == FOUND and (r.global_idx, list(r.secret)) == (exp[1], list(exp[0]))) if exp else \
+                r.status == EXHAUSTED, (nonce, k0, r, exp)
+
+
 def test_random_windows_vs_oracle(miner, oracle):
     """Random nonces, partitions and windows (hits and misses), oracle-sized."""
     rnd = random.Random(416)

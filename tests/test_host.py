@@ -52,12 +52,22 @@ def test_thread_bytes_mirror(oracle):
 
 def test_plan_window_segments():
     pl = distpow.plan_window(b"\x01\x02\x03\x04", 0, 0, 0, (1 << 24) + 5)
-    spans = [(p.k_begin, p.k_end, p.chunk_len) for p in pl]
-    assert spans == [(0, 1, 0), (1, 256, 1), (256, 65536, 2), (65536, 1 << 24, 3),
-                     (1 << 24, (1 << 24) + 5, 4)]
+    spans = [(p.k_begin, p.k_end, p.chunk_len, p.chunk_len_last, p.start_kernel) for p in pl]
+    # k = 0 in the start kernel; chunk lengths 1..3 in one launch (SH = 0); then L = 4
+    assert spans == [(0, 1, 0, 0, 1), (1, 1 << 24, 1, 3, 0), (1 << 24, (1 << 24) + 5, 4, 4, 0)]
     for p in pl:
         assert (p.nblk, p.w0, p.sh) == (1, 1, 0)  # 4-byte nonce: V lands in word 1
         assert p.i_begin == p.k_begin * 256 and p.i_end == p.k_end * 256
+    # a window inside the merged range, and one from k = 300
+    assert [(p.k_begin, p.k_end) for p in distpow.plan_window(b"\x01\x02\x03\x04", 0, 0, 200, 70000)] == \
+        [(200, 70000)]
+    # SH != 0 layouts and R = 1 (workerBits 8) keep one launch per chunk length
+    for nonce, wb, wbits in ((b"abc", 0, 0), (b"abcde", 0, 0), (b"abcd", 3, 8)):
+        assert [(p.k_begin, p.k_end, p.chunk_len) for p in distpow.plan_window(nonce, wb, wbits, 0, 70000)] == \
+            [(0, 1, 0), (1, 256, 1), (256, 65536, 2), (65536, 70000, 3)], nonce
+    # 52-byte nonce (W0 = 13, SH = 0): chunk length 3 needs a second block -- merged up to it
+    pl = distpow.plan_window(bytes(52), 0, 0, 0, 70000)
+    assert [(p.k_begin, p.k_end, p.nblk) for p in pl] == [(0, 1, 1), (1, 65536, 1), (65536, 70000, 2)]
     # L >= 4: one launch spans the 2^24-k segments (the kernel re-derives the constants
     # of the words holding k >> 24); windows split only where the chunk length changes
     pl = distpow.plan_window(b"ab", 2, 2, (3 << 24) - 7, (5 << 24) + 3)

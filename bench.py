@@ -105,7 +105,19 @@ def main():
             dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)
     board = None
     if world > 1 and NODE_BOARD:
-        board = NodeBoard.create()  # None when the ranks do not share one host
+        try:
+            board = NodeBoard.create()  # None when the ranks do not share one host
+        except Exception as e:  # the node search stays correct without it (batch boundaries only)
+            log(f"rank {rank}: no node board ({e!r}); node_mine runs on batch boundaries alone")
+            board = None
+        # every rank must agree on using it (node_mine's collectives stay matched either way,
+        # but the board's slot reset schedule assumes all ranks call it)
+        have = torch.tensor([1 if board is not None else 0], dtype=torch.int64,
+                            device=torch.device("cuda", device) if args.backend == "nccl" else "cpu")
+        dist.all_reduce(have, op=dist.ReduceOp.MIN)
+        if int(have.item()) == 0 and board is not None:
+            board.close()
+            board = None
     wb, wbits = partition_of_rank(rank, world)
     R = 1 << (8 - wbits)
     per_gpu = (STRONG_TOTAL_PER_STEP // world) if args.strong else CANDIDATES_PER_GPU_PER_STEP

@@ -708,6 +708,7 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
     PlannedLaunch pl;
     size_t n = 0;
     while (planner.next(pl)) {
+        if (pl.k0) continue;  // k = 0: the search's start kernel, not an md5 launch
         uint64_t wblocks = 0;
         const int r = size_launch(pl, max_blocks, ~0ull, &wblocks);
         if (r < 0) return set_error(r, "dpow_diag_launch_geometry: launch grid leaves a claim counter without waves");

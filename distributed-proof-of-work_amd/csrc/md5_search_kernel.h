@@ -772,7 +772,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
             if (!EQ && m != 0) m &= __ballot((dig[3][j] & L.dmask) == 0u);
             if (m != 0 && L.ntz > 8u) {
                 uint32_t d0, sd[3];
-                seg_all_deltas<NBLK, W0, SH>(L, seg_id(ij >> L.rbits), d0, sd);
+                seg_all_deltas<NBLK, W0, SH>(L, seg_id((ij < L.i_begin ? L.i_begin : ij) >> L.rbits), d0, sd);
                 const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, kc, vs[j], loff, sd);
                 m = __ballot(ok);
             }
@@ -937,7 +937,9 @@ DPOW_DEV void search_body(const Launch &L) {
             // constants.  (Splitting groups at boundaries in the kernel instead
             // costs 4 SGPR spill reloads per wave-block: tools/isa_loop.py.)
             {
-                const uint32_t sg = seg_id(i0 >> L.rbits);
+                // (from the launch's first index: a wave-block below it may hold k = 0, whose
+                // lanes are masked off and whose chunk length differs from its neighbours')
+                const uint32_t sg = seg_id((i0 < L.i_begin ? L.i_begin : i0) >> L.rbits);
                 if (sg != __builtin_amdgcn_readfirstlane(cur_seg_v)) {
                     asm volatile("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(sg));
                     uint32_t d0, d[3];

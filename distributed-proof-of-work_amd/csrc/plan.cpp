@@ -201,6 +201,7 @@ void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words
     if (sh) words[w0 + 1] += V >> (32 - 8 * sh);
     if (Lh.seg0 == kLsegBase && !pl.k0) {  // SH = 0 below 2^24: md5_search_kernel.h seg_all_deltas
         uint32_t d0, d1, dlen;
+        // (the kernel takes a group's chunk length from its first index at or above i_begin)
         lseg_deltas(chunk_len_of(local_idx >> Lh.rbits), d0, d1, dlen);
         const uint32_t lenw = 16 * pl.info.nblk - 2;
         if (w0 + 1 == lenw) {

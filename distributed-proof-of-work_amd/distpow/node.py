@@ -50,7 +50,11 @@ def owner_rank(global_idx: int, world: int) -> int:
 
 
 RANK_RATE = 2.17e11        # candidates/s of one MI355X on the one-block layouts (bench `value`)
-BATCH_OVERHEAD_S = 1e-4    # node_mine's fixed cost per batch: window launch + drain, all-reduce, host copies
+# node_mine's fixed cost per batch c: the window's search call (start kernel, launch, drain,
+# completion record) plus the batch boundary (pinned copy in, all-reduce MIN, copy out,
+# synchronize).  Measured on an MI355X over a world-1 RCCL group (tests/test_gpu_rccl.py,
+# bench.py `collective`): boundary 31-33 us, a whole batch of 2^16 candidates 74-80 us.
+BATCH_OVERHEAD_S = 8e-5
 
 
 def auto_batch_candidates(num_trailing_zeros: int, world: int, rate: float = RANK_RATE,

@@ -53,6 +53,22 @@ def check(d, max_blocks):
     assert holders <= d.worker_blocks <= max(max_blocks, CLAIM_COUNTERS)
     # no more workgroups than the claims need (one wave per claim, rounded up to a workgroup)
     assert d.worker_blocks <= max(-(-d.n_chunks // WPB), holders)
+    # a launch spanning chunk lengths 1..3 (plan.cpp lspan): no claim straddles k = 256 or
+    # 65536 (the kernel takes a claim group's chunk length from its first index >= i_begin)
+    def clen(k):
+        return (k > 0) + (k > 0xFF) + (k > 0xFFFF)
+    if d.k_begin < (1 << 24) and clen(d.k_begin) != clen(d.k_end - 1):
+        assert d.k_begin >= 1 and d.rbits >= 1
+        assert d.chunk & (d.chunk - 1) == 0 and d.chunk % d.chunk_tail == 0 and d.chunk <= 2 << d.rbits
+        assert d.wb_begin % (d.chunk * W) == 0
+        for b in (256 << d.rbits, 65536 << d.rbits):  # local index of the boundary
+            if not d.i_begin < b < d.i_end:
+                continue
+            wbb = (b - d.wb_begin) // W  # its wave-block, which must start a claim
+            assert (b - d.wb_begin) % W == 0
+            big = d.n_big * d.chunk
+            assert (wbb % d.chunk == 0) if wbb < big else ((wbb - big) % d.chunk_tail == 0), \
+                (d.k_begin, d.k_end, d.rbits, b)
     seg_i = 1 << (24 + d.rbits)  # local indices per 2^24-k segment
     if d.k_begin >> 24 != (d.k_end - 1) >> 24:
         assert d.chunk & (d.chunk - 1) == 0 and d.chunk % d.chunk_tail == 0
@@ -97,6 +113,23 @@ def test_large_and_small_windows():
             for nonce in ([1, 2, 3, 4], [1, 2]):  # SH 0; SH 2 (word W0+2 splits at L = 6)
                 for d in geometry(nonce, wb, wbits, k0, k1, max_blocks):
                     check(d, max_blocks)
+
+
+def test_chunk_length_spanning_launches():
+    """Windows across k = 1, 256 and 65536 for SH = 0 nonces: one md5 launch spans the chunk
+    lengths (after the start kernel's k = 0), and its claims respect the boundaries."""
+    rnd = random.Random(7)
+    for _ in range(300):
+        wbits = rnd.choice([0, 1, 2, 3, 5, 7])
+        wb = rnd.randrange(1 << wbits) if wbits else 0
+        k0 = rnd.choice([0, 1, 2, 200, 255, 256, 300, 65000, 65535])
+        k1 = min(1 << 24, k0 + rnd.choice([2, 60, 300, 5000, 70000, 1 << 20, 1 << 24]))
+        nonce = [rnd.randrange(256) for _ in range(rnd.choice([0, 4, 8, 44, 48, 60, 64]))]
+        ds = geometry(nonce, wb, wbits, k0, k1, rnd.choice([8, 768, 1536]))
+        assert len(ds) == 1, (len(nonce), k0, k1, [(d.k_begin, d.k_end) for d in ds])
+        assert ds[0].k_begin == max(k0, 1) and ds[0].k_end == k1
+        for d in ds:
+            check(d, 1536)
 
 
 def test_bench_step_is_one_launch():

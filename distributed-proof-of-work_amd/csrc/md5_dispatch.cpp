@@ -6,6 +6,11 @@ namespace dpow {
 hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream,
                          hipEvent_t start, hipEvent_t stop) {
     if (!variant_exists(nblk, w0, sh)) return hipErrorInvalidValue;
+    if (L.seg0 == kLsegBase) {
+        if (sh != 0) return hipErrorInvalidValue;
+        return nblk == 1 ? variant_launch_1_0_ls(w0, L, grid, stream, start, stop)
+                         : variant_launch_2_0_ls(w0, L, grid, stream, start, stop);
+    }
 #define DPOW_CASE(n, s) \
     if (nblk == n && sh == s) return variant_launch_##n##_##s(w0, L, grid, stream, start, stop);
     DPOW_CASE(1, 0) DPOW_CASE(1, 1) DPOW_CASE(1, 2) DPOW_CASE(1, 3)

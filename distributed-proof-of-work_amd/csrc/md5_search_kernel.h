@@ -31,7 +31,23 @@
 
 #include "dpow_common.h"
 
+// DPOW_VLS = 1 (md5_variant.hip's "_ls" translation units): the SH = 0 kernels of launches
+// below k = 2^24, whose template is chunk length 0's and which may span chunk lengths 1..3
+// (Launch::seg0 == kLsegBase): the pad word W0 + 1 and the bit-length word are segment
+// words.  0: every other launch.  Separate kernels, in their own namespace: holding the
+// bit-length word's K + M in VGPRs cost the sweep kernel 2 % through register assignment
+// alone, with an identical instruction count (217.3 -> 214.0 GH/s, profiles/r03_ab_lspan.log).
+#ifndef DPOW_VLS
+#define DPOW_VLS 0
+#endif
+#if DPOW_VLS
+#define DPOW_KNS lsk
+#else
+#define DPOW_KNS k
+#endif
+
 namespace dpow {
+namespace DPOW_KNS {
 
 #define DPOW_DEV __device__ __forceinline__
 #define DPOW_DEV_CONST __host__ __device__ constexpr
@@ -143,7 +159,7 @@ struct KConst {
 template <int NBLK, int W0, int SH>
 DPOW_DEV_CONST bool seg_word(int m) {
     return (DPOW_SPAN && ((SH == 0 && m == W0 + 1) || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2))) ||
-           (DPOW_LSPAN && SH == 0 && (m == W0 + 1 || m == 16 * NBLK - 2));
+           (DPOW_VLS && SH == 0 && (m == W0 + 1 || m == 16 * NBLK - 2));
 }
 
 // First hand-ordered step of block 0: W0 + pipe_lead<NBLK, W0, SH>.  4 is the first
@@ -272,7 +288,7 @@ template <int NBLK, int W0, int SH>
 DPOW_DEV void seg_all_deltas(const Launch &L, uint32_t sg, uint32_t &d0, uint32_t (&d)[3]) {
     d0 = d[0] = d[1] = d[2] = 0u;
     if (sg >= kLsegBase) {
-        if constexpr (SH == 0 && DPOW_LSPAN) {
+        if constexpr (SH == 0 && DPOW_VLS) {
             lseg_deltas((sg - kLsegBase) & 3u, d0, d[0], d[2]);
             if constexpr (W0 + 1 == 16 * NBLK - 2) {  // W0 + 1 is the bit-length word
                 d[2] += d[0];
@@ -1038,4 +1054,5 @@ md5_search_kernel_lsgpr(const Launch L) {
     search_body<NBLK, W0, SH, EQ>(L);
 }
 
+}  // namespace DPOW_KNS
 }  // namespace dpow

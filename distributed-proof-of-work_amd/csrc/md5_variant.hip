@@ -17,6 +17,7 @@
 namespace dpow {
 
 namespace {
+using namespace DPOW_KNS;
 using KernelFn = void (*)(Launch);
 // [EQ][w0 - kW0Lo]: EQ kernels (the D-equality test, use_d_equality) exist for
 // one final block only.
@@ -48,8 +49,14 @@ KernelFn pick(int w0, bool eq) {
 }
 }  // namespace
 
-#define DPOW_CAT3(a, b, c) a##b##_##c
-#define DPOW_NAME(a, b, c) DPOW_CAT3(a, b, c)
+#if DPOW_VLS  // the chunk-length-spanning SH = 0 kernels: variant_launch_<n>_0_ls
+#define DPOW_SFX _ls
+#else
+#define DPOW_SFX
+#endif
+#define DPOW_CAT4(a, b, c, d) a##b##_##c##d
+#define DPOW_NAME2(a, b, c, d) DPOW_CAT4(a, b, c, d)
+#define DPOW_NAME(a, b, c) DPOW_NAME2(a, b, c, DPOW_SFX)
 
 hipError_t DPOW_NAME(variant_launch_, DPOW_VNBLK, DPOW_VSH)(int w0, const Launch &L, uint32_t grid,
                                                            hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
@@ -68,11 +75,11 @@ hipError_t DPOW_NAME(variant_occupancy_, DPOW_VNBLK, DPOW_VSH)(int w0, int *bloc
 
 }  // namespace dpow
 
-#if DPOW_WAVE_TRACE && DPOW_VNBLK == 1 && DPOW_VSH == 0
+#if DPOW_WAVE_TRACE && DPOW_VNBLK == 1 && DPOW_VSH == 0 && !DPOW_VLS
 // Diagnostic builds only: the per-wave trace of the last one-block, SH = 0 launch.
 extern "C" int dpow_diag_wave_trace(unsigned long long *out, size_t n) {
-    if (n > dpow::kTraceWaves * 4) n = dpow::kTraceWaves * 4;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(dpow::g_wave_trace), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+    if (n > dpow::DPOW_KNS::kTraceWaves * 4) n = dpow::DPOW_KNS::kTraceWaves * 4;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(dpow::DPOW_KNS::g_wave_trace), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
                ? 0
                : -2;
 }

@@ -19,6 +19,8 @@ DPOW_DECL_VARIANT(2, 0)
 DPOW_DECL_VARIANT(2, 1)
 DPOW_DECL_VARIANT(2, 2)
 DPOW_DECL_VARIANT(2, 3)
+DPOW_DECL_VARIANT(1, 0_ls)  // chunk-length-spanning SH = 0 kernels (launches below k = 2^24)
+DPOW_DECL_VARIANT(2, 0_ls)
 #undef DPOW_DECL_VARIANT
 
 // True when a kernel variant exists for (nblk, w0, sh).
@@ -31,6 +33,8 @@ inline bool variant_exists(int nblk, int w0, int sh) {
 
 // start / stop (may be null): timing events recorded by the kernel's own dispatch
 // packet (hipExtLaunchKernel), not as separate marker packets between launches.
+// Launches whose template is chunk length 0's (L.seg0 == kLsegBase: SH = 0 below k = 2^24)
+// run the "_ls" kernels.
 hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream,
                          hipEvent_t start, hipEvent_t stop);
 hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu);

@@ -19,10 +19,10 @@ def main(trace_csv, tts_json):
     searches, cur = [], None
     for r in rows:
         name = r["Kernel_Name"]
-        if "search_reset" in name:
+        if ("search_reset" in name or "search_start" in name):
             cur = []
             searches.append(cur)
-        if cur is not None and ("search_reset" in name or "md5_search" in name):
+        if cur is not None and (("search_reset" in name or "search_start" in name) or "md5_search" in name):
             cur.append(r)
     host = json.load(open(tts_json))
     searches = searches[len(searches) - len(host):]  # drop the warm-up search(es)
@@ -33,7 +33,7 @@ def main(trace_csv, tts_json):
         prev_end = None
         for r in ks:
             s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-            launches.append({"kernel": "search_reset" if "search_reset" in r["Kernel_Name"] else "md5_search",
+            launches.append({"kernel": "search_reset" if ("search_reset" in r["Kernel_Name"] or "search_start" in r["Kernel_Name"]) else "md5_search",
                              "start_us": round((s - t0) / 1e3, 1), "dur_us": round((e - s) / 1e3, 1),
                              "gap_us": None if prev_end is None else round((s - prev_end) / 1e3, 1),
                              "grid_threads": int(r["Grid_Size_X"]) if "Grid_Size_X" in r else int(r.get("Grid_Size", 0))})

@@ -670,10 +670,11 @@ int dpow_verify(const uint8_t *nonce, size_t nonce_len, const uint8_t *secret, s
     return digest_trailing_zero_nibbles(d) >= ntz ? 1 : 0;
 }
 
-int dpow_plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte, uint32_t worker_bits,
-                     uint64_t k_begin, uint64_t k_end, dpow_plan_launch *out, size_t max_launches) {
+int dpow_plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
+                     uint32_t worker_bits, uint64_t k_begin, uint64_t k_end, dpow_plan_launch *out,
+                     size_t max_launches) {
     std::vector<PlannedLaunch> plan;
-    int n = plan_window(nonce, nonce_len, 0, worker_byte, worker_bits, k_begin, k_end, plan);
+    int n = plan_window(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end, plan);
     if (n < 0) return set_error(n, "dpow_plan_window: bad arguments");
     for (size_t i = 0; i < plan.size() && i < max_launches && out; ++i) out[i] = plan[i].info;
     return n;

@@ -62,6 +62,7 @@ int WindowPlanner::init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, ui
     p_ = (uint32_t)(nonce_len % 64);
     k_ = k_begin;
     k_end_ = k_end;
+    lspan_ok_ = lspan_layout(nonce_len, rbits_, ntz);
     // Midstate over nonce-only blocks.
     for (int w = 0; w < 4; ++w) iv_[w] = kMd5IV[w];
     for (size_t b = 0; b < blk_v_; ++b) {
@@ -93,15 +94,19 @@ void WindowPlanner::build_template(uint64_t k, uint32_t L, uint32_t nblk, uint32
     for (uint32_t w = 0; w < 32; ++w) T[w] = w < 16 * nblk ? load_le32(buf + 4 * w) : 0u;
 }
 
-bool lspan_layout(size_t nonce_len, uint32_t rbits) {
+bool lspan_layout(size_t nonce_len, uint32_t rbits, uint32_t ntz) {
     // SH = 0: the pads of chunk lengths 0..3 fall in words W0 / W0 + 1, whose K + M the
     // kernel re-derives per segment.  R >= 2: a power-of-two chunk of <= 2R wave-blocks puts
     // the boundaries k = 256 and 65536 (256 R and 65536 R indices) on claim boundaries.
-    return DPOW_LSPAN && nonce_len % 4 == 0 && rbits >= 1;
+    // A first hit expected within kLspanMaxExpect candidates: the spanning (_ls) kernels
+    // hash 1.5-2 % slower than the per-length ones (register assignment), which outweighs
+    // the two launches they save (~40 us) once the search is expected to run > ~1.5 ms
+    // ([1,2,3,4]/8: 19.18 -> 19.45 ms merged, profiles/r03_ab_lspan.log).
+    return DPOW_LSPAN && nonce_len % 4 == 0 && rbits >= 1 && expected_first_hit(ntz, rbits) <= kLspanMaxExpect;
 }
 
 bool WindowPlanner::lseg_template(uint64_t k) const {
-    return DPOW_LSPAN && p_ % 4 == 0 && k < (1ull << 24);
+    return lspan_ok_ && k < (1ull << 24);
 }
 
 bool WindowPlanner::next(PlannedLaunch &pl) {
@@ -121,7 +126,7 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     pl.k0 = DPOW_START_K0 && k == 0;
     // (the start kernel hashes k = 0 from the real chunk-length-0 template: no deltas)
     uint32_t L_last = L;
-    if (!pl.k0 && k >= 1 && k < (1ull << 24) && lspan_layout(nonce_len_, rbits_)) {
+    if (!pl.k0 && k >= 1 && lseg_template(k)) {
         // Merge the following chunk lengths (up to 3) with the same block count.
         uint64_t e = ke;
         while (e < k_end_ && e < (1ull << 24) && nblk_of(chunk_len_of(e)) == nblk) {

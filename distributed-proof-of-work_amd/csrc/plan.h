@@ -25,7 +25,8 @@ uint64_t segment_end(uint64_t k);
 uint64_t word2_period(uint32_t sh);
 // The planner may merge chunk lengths 1..3 (k in [1, 2^24)) into one launch: SH = 0
 // layouts, R >= 2, equal block counts (WindowPlanner::next).
-bool lspan_layout(size_t nonce_len, uint32_t rbits);
+constexpr uint64_t kLspanMaxExpect = 1ull << 28;
+bool lspan_layout(size_t nonce_len, uint32_t rbits, uint32_t ntz);
 #ifndef DPOW_START_K0
 #define DPOW_START_K0 1  // k = 0 hashed by the search's start kernel (A/B switch)
 #endif
@@ -48,6 +49,7 @@ class WindowPlanner {
     size_t nonce_len_ = 0, blk_v_ = 0;
     uint32_t p_ = 0, ntz_ = 0, rbits_ = 0, base_tb_ = 0;
     uint64_t k_ = 0, k_end_ = 0;
+    bool lspan_ok_ = false;  // launches below k = 2^24 use the chunk-length-0 template and may span
     uint32_t iv_[4] = {0, 0, 0, 0};
 };
 

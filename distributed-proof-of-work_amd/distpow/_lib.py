@@ -164,7 +164,7 @@ def lib():
         "dpow_trailing_zero_nibbles": (ctypes.c_uint32, [ctypes.c_char_p]),
         "dpow_verify": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                        ctypes.c_uint32]),
-        "dpow_plan_window": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+        "dpow_plan_window": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(PlanLaunch),
                                             ctypes.c_size_t]),
         "dpow_plan_candidate": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,

@@ -73,12 +73,13 @@ def verify(nonce, secret, num_trailing_zeros: int) -> bool:
     return lib().dpow_verify(n, len(n), s, len(s), num_trailing_zeros) == 1
 
 
-def plan_window(nonce, worker_byte, worker_bits, k_begin, k_end) -> List[PlanLaunch]:
+def plan_window(nonce, worker_byte, worker_bits, k_begin, k_end, num_trailing_zeros: int = 0) -> List[PlanLaunch]:
+    """The launches dpow_search would queue for this window (dpow_plan_window)."""
     n = _b(nonce)
-    cnt = check(lib().dpow_plan_window(n, len(n), worker_byte, worker_bits, k_begin, k_end, None, 0),
-                "dpow_plan_window")
+    cnt = check(lib().dpow_plan_window(n, len(n), num_trailing_zeros, worker_byte, worker_bits, k_begin, k_end,
+                                       None, 0), "dpow_plan_window")
     arr = (PlanLaunch * max(cnt, 1))()
-    check(lib().dpow_plan_window(n, len(n), worker_byte, worker_bits, k_begin, k_end, arr, cnt),
+    check(lib().dpow_plan_window(n, len(n), num_trailing_zeros, worker_byte, worker_bits, k_begin, k_end, arr, cnt),
           "dpow_plan_window")
     return list(arr[:cnt])
 

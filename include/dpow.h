@@ -155,7 +155,8 @@ int dpow_verify(const uint8_t *nonce, size_t nonce_len, const uint8_t *secret,
                 size_t secret_len, uint32_t ntz);
 
 /* Launch plan of a window (host logic of dpow_search, exposed for testing):
- * one entry per kernel launch.  Returns the number of launches (may exceed
+ * one entry per kernel launch, as dpow_search with these arguments would queue them
+ * (ntz matters: chunk lengths 1..3 share a launch only when a hit is expected early).  Returns the number of launches (may exceed
  * max_launches, in which case only the first max_launches are written), or a
  * negative error code. */
 typedef struct dpow_plan_launch {
@@ -167,7 +168,7 @@ typedef struct dpow_plan_launch {
     uint32_t chunk_len_last;   /* ... and of k_end - 1 (one launch may span chunk lengths 1..3) */
     uint32_t start_kernel;     /* 1: k = 0, hashed by the search's start kernel, not an md5 launch */
 } dpow_plan_launch;
-int dpow_plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte,
+int dpow_plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
                      uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,
                      dpow_plan_launch *out, size_t max_launches);
 

@@ -56,7 +56,7 @@ int main(int argc, char **argv) {
     if (d[0] != 0x90 || d[15] != 0x72) return fail("dpow_md5 (RFC 1321 'abc')");
     if (dpow_trailing_zero_nibbles(d) != 0) return fail("dpow_trailing_zero_nibbles");
     dpow_plan_launch plan[8];
-    const int n = dpow_plan_window(nonce, sizeof nonce, 0, 0, 0, (1u << 24) + 5, plan, 8);
+    const int n = dpow_plan_window(nonce, sizeof nonce, 0, 0, 0, 0, (1u << 24) + 5, plan, 8);
     /* k = 0 (start kernel), k in [1, 2^24) (chunk lengths 1..3 in one launch), then L = 4 */
     if (n != 3 || !plan[0].start_kernel || plan[1].chunk_len != 1 || plan[1].chunk_len_last != 3 ||
         plan[2].chunk_len != 4)

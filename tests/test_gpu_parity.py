@@ -544,9 +544,13 @@ def test_bound_beyond_a_chunk_length_split(miner, golden):
     segment after the L = 2 one: the window splits at k = 2^16) still hold candidates
     below it, among them this search's own first hit.  The bound is the node slot's best
     at the search's start (deterministic: the first launch's record already shows it)."""
-    e7 = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 7)
-    g7 = e7["global_idx"]  # k = 905,898: in the L = 3 launch of a window from k = 256
+    e7 = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 8)
+    g7 = e7["global_idx"]  # k = 15,880,380: in the L = 3 launch of a window from k = 256
     assert (g7 >> 8) > (1 << 16)
+    # N = 8 expects its first hit too late to merge chunk lengths 2 and 3 into one launch
+    # (plan.cpp lspan_layout): the window is two launches, split at k = 2^16
+    assert [(p.k_begin, p.k_end) for p in distpow.plan_window([1, 2, 3, 4], 0, 0, 256, 1 << 24, 8)] == \
+        [(256, 1 << 16), (1 << 16, 1 << 24)]
     slot = _Slot()
     lib = distpow.lib()
     addr = ctypes.addressof(slot)
@@ -558,7 +562,7 @@ def test_bound_beyond_a_chunk_length_split(miner, golden):
                         (((1 << 16) - 7) << 8, (EXHAUSTED, None))):  # inside launch 0
             lib.dpow_node_slot_reset(addr)
             lib.dpow_node_post(addr, b)
-            r = miner.search([1, 2, 3, 4], 7, 0, 0, 256, 1 << 24)
+            r = miner.search([1, 2, 3, 4], 8, 0, 0, 256, 1 << 24)
             assert (r.status, r.global_idx if r.status == FOUND else None) == want, (b, r)
             # a hit is posted to the slot (atomic min); a bounded search leaves it alone
             assert slot.best == (min(b, g7) if r.status == FOUND else b) and slot.stop == 0
@@ -571,7 +575,7 @@ def test_bound_beyond_a_chunk_length_split(miner, golden):
     finally:
         miner.attach_node(None)
     # detached: the same window finds the hit without any bound
-    r = miner.search([1, 2, 3, 4], 7, 0, 0, 256, 1 << 24)
+    r = miner.search([1, 2, 3, 4], 8, 0, 0, 256, 1 << 24)
     assert r.status == FOUND and r.global_idx == g7
 
 

@@ -38,7 +38,7 @@ SWEEP_NTZ = 32
 CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 STRONG_TOTAL_PER_STEP = 1 << 38    # --strong: fixed total work per step
 K0 = 1 << 24                      # start of the L = 4 segment
-PROFILE_TAG = "r02"                # profiles/<tag>_summary.json of the current kernel
+PROFILE_TAG = "r03"                # profiles/<tag>_summary.json of the current kernel
 # time-to-secret at N > 1: node_mine's constant per-rank batch sized for N and the node (node.auto_batch_candidates)
 TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first_ms: the first, cold)
 # N > 1 time-to-secret: node_mine (batch-synchronous, RCCL all-reduce at batch boundaries,

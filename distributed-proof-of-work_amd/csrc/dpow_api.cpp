@@ -80,8 +80,11 @@ constexpr size_t kClaimRing = 64;
 constexpr size_t kDepth = 3;
 static_assert(kDepth < kClaimRing, "a claim slot is reused only after its launch completed");
 constexpr size_t kRing = 8;  // completion records and event pairs, indexed by launch seq (>= kDepth + 1)
-// Word of the pinned cancel page holding the stale launch sequence (Launch::stale).
+// Words of the pinned cancel page: the stale launch sequence (Launch::stale) and the
+// 64-bit bound injected by dpow_search_bound (Launch::ext_bound, relayed by the watcher).
 constexpr size_t kStaleWord = 8;
+constexpr size_t kBoundWord = 16;  // uint32 index of an 8-byte-aligned 64-bit word
+constexpr size_t kCancelPage = 128;
 // Completion-record wait: spin for the first kSpinNs of a search (time-to-secret),
 // then poll at kPollNs (20 us in round 2: a record waited up to that long to be seen,
 // profiles/r03_stop_latency.json; the thread sleeps between polls either way).
@@ -114,14 +117,15 @@ struct ActiveSearch {
     ~ActiveSearch() { g_active[dev].fetch_sub(1, std::memory_order_relaxed); }
 };
 
-// Timing of one queued launch (its HIP events), harvested into dpow_stats
-// lazily -- never on the path between a hit and dpow_search returning.
+// One queued launch: its completion record slot (seq % kRing) and what its record adds
+// to dpow_stats once consumed (launches, candidates, and the kernel time the launch
+// stamps into the record itself).
 struct LaunchSlot {
-    hipEvent_t start = nullptr, end = nullptr;
-    bool pending = false;  // events recorded, not yet harvested
-    bool counted = false;  // its completion record was consumed: its work counts in the stats
+    uint64_t seq = 0;       // launch sequence number of the slot's last user
+    bool in_flight = false; // its record was not consumed: it may still be running
     uint64_t candidates = 0;
     uint64_t g_end = 0;    // global indices of this launch are below g_end = k_end * 256
+    hipStream_t stream = nullptr;  // the stream it was queued on (the k = 0 kernel: the second one)
 };
 
 int64_t now_ns() {
@@ -157,66 +161,53 @@ struct SearchWait {
 struct dpow_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    Ctrl *d_ctrl = nullptr;
+    Ctrl *d_ctrl = nullptr;  // kCtrlRing control blocks (kCtrlStride apart); ctrl_idx's is clean
+    uint32_t ctrl_idx = 0;
     unsigned long long *d_claims = nullptr;  // kClaimRing slots of kClaimSlot claim counters
     Snap *h_snap = nullptr;        // kRing completion records: pinned, host-coherent, mapped
     Snap *d_snap = nullptr;        // device alias
-    uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped: [0] the cancel flag, [kStaleWord] stale seq
+    uint32_t *h_cancel = nullptr;  // pinned, host-coherent, mapped: [0] the cancel flag, [kStaleWord] stale seq,
+                                   //  [kBoundWord] the injected bound (64-bit)
     uint32_t *d_cancel = nullptr;  // device alias
     uint32_t cus = 0;
     uint64_t seq = 0;  // launches ever queued on this context (record/slot index = seq % kRing)
     LaunchSlot slots[kRing];
     dpow_stats stats{};
     // External bound (dpow_search_bound): lowered from another thread while a
-    // search runs, applied to Ctrl::best by a one-thread atomicMin kernel on
-    // bound_stream, ordered after the search's reset kernel (reset_ev).
+    // search runs, written to the pinned bound word, which the running launch's
+    // watcher relays to Ctrl::best (as it relays the node slot's best).
     std::mutex bound_mu;
     bool searching = false;                      // under bound_mu
     std::atomic<uint64_t> ext_bound{DPOW_NO_HIT};  // the lowest bound injected into the running search
-    hipStream_t bound_stream = nullptr;
-    hipEvent_t reset_ev = nullptr;
-    hipEvent_t reset_done = nullptr;  // the running search's start kernel is done (reset_ev, or its timing event)
+    hipStream_t aux_stream = nullptr;  // the k = 0 kernel, beside the search's first md5 launch
     // Node slot (dpow_node_attach): shared by the ranks of one node, polled while a
     // search waits for its records.
     dpow_node_slot *node = nullptr;
     dpow_node_slot *d_node = nullptr;  // its device alias (the watcher polls it)
     std::vector<void *> registered;    // host pages registered for the node slots attached so far
     uint32_t poll_override = 0;  // DPOW_DIAG_POLL_WB (A/B runs): wave-blocks per poll group for every launch
+    uint32_t bpc_override = 0;   // DPOW_DIAG_BPC: worker workgroups per CU for every launch
+    uint32_t min_chunk_override = 0;  // DPOW_DIAG_MIN_CHUNK: minimum wave-blocks per claim (a power of two)
+    int64_t diag_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // the last search's host timeline (dpow_diag_search_times)
 };
 
 namespace {
 
-// Fold one launch's kernel time into the stats.  Its end event is long
-// complete by the time a slot is reused, so the synchronisation is immediate.
-int harvest(dpow_ctx *c, LaunchSlot &s) {
-    if (!s.pending) return 0;
-    s.pending = false;
-    DPOW_HIP(hipEventSynchronize(s.end));
-    if (!s.counted) return 0;
-    float ms = 0.f;
-    DPOW_HIP(hipEventElapsedTime(&ms, s.start, s.end));
-    c->stats.launches++;
-    c->stats.candidates += s.candidates;
-    c->stats.kernel_ms += ms;
-    return 0;
-}
+// Before a record slot is reused: a launch whose record was never consumed (queued behind
+// a hit, a cancel or an error, possibly on the other stream) may still be running; wait
+// for its record, so it cannot land on the slot's next user.
+int retire_slot(dpow_ctx *c, LaunchSlot &s);
 
-int harvest_all(dpow_ctx *c) {
-    for (LaunchSlot &s : c->slots)
-        if (harvest(c, s) < 0) return DPOW_EHIP;
-    return 0;
-}
+uint64_t *bound_word(dpow_ctx *c) { return reinterpret_cast<uint64_t *>(c->h_cancel + kBoundWord); }
 
-// Lower Ctrl::best of the running search to g (dpow_search_bound, and the node
-// slot's best): a one-thread atomicMin kernel on the bound stream, ordered after
-// the search's reset kernel.  The caller holds bound_mu.
+// Lower Ctrl::best of the running search to g (dpow_search_bound): the pinned bound
+// word, which the running launch's watcher relays to Ctrl::best within its poll (about
+// 1 us).  Round 2 launched a one-thread atomicMin kernel on a second stream instead,
+// which took 50-160 us to start beside the running grid.  The caller holds bound_mu.
 int inject_bound_locked(dpow_ctx *c, uint64_t g) {
     if (g >= c->ext_bound.load(std::memory_order_relaxed)) return 0;
     c->ext_bound.store(g, std::memory_order_release);
-    DPOW_HIP(hipSetDevice(c->device));
-    DPOW_HIP(hipStreamWaitEvent(c->bound_stream, c->reset_done, 0));  // after this search's reset
-    const hipError_t e = search_bound(c->d_ctrl, g, c->bound_stream);
-    if (e != hipSuccess) return hip_fail(e, "search_bound");
+    __atomic_store_n(bound_word(c), g, __ATOMIC_RELEASE);
     return 0;
 }
 
@@ -257,7 +248,7 @@ int wait_record(dpow_ctx *c, uint64_t seq, int64_t deadline, SearchWait &sw) {
         if (t >= deadline) return 0;
         const bool spinning = t - sw.t0 < kSpinNs;
         if (spinning ? (it % 4096 == 0) : (it % 16 == 0)) {
-            const hipError_t q = hipStreamQuery(c->stream);
+            const hipError_t q = hipStreamQuery(c->slots[seq % kRing].stream);
             if (q == hipSuccess) {
                 if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 1;
                 return set_error(DPOW_EHIP, "dpow_search: stream idle without the launch's completion record");
@@ -278,6 +269,25 @@ int wait_record(dpow_ctx *c, uint64_t seq, int64_t deadline, SearchWait &sw) {
             nanosleep(&ts, nullptr);
         }
     }
+}
+
+int retire_slot(dpow_ctx *c, LaunchSlot &s) {
+    if (!s.in_flight) return 0;
+    const uint32_t *p = &c->h_snap[s.seq % kRing].seq;
+    const uint32_t want = (uint32_t)(s.seq + 1);
+    for (uint64_t it = 1; __atomic_load_n(p, __ATOMIC_ACQUIRE) != want; ++it) {
+        if (it % 1024 == 0) {
+            const hipError_t q = hipStreamQuery(s.stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) break;
+                return set_error(DPOW_EHIP, "dpow_search: stream idle without a queued launch's completion record");
+            }
+            if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
+        }
+        __builtin_ia32_pause();
+    }
+    s.in_flight = false;
+    return 0;
 }
 
 // The body of dpow_search (arguments checked).
@@ -304,18 +314,33 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     const uint64_t node_best = c->node ? __atomic_load_n(&c->node->best, __ATOMIC_ACQUIRE) : DPOW_NO_HIT;
     sw.node_seen = node_best;
     const uint64_t seq0 = c->seq;
+    for (int64_t &t : c->diag_t) t = -1;
     size_t launched = 0, consumed = 0;
     int64_t busy_until = 0;  // expected end of the launches queued so far (now_ns clock)
     PlannedLaunch pl;
     bool have = planner.next(pl);
-    // The start kernel resets the control block and claim counters; when the window holds
-    // k = 0 it also hashes those R candidates (search_ctrl.hip) and counts as launch 0 of
-    // the search, with a completion record of its own.
+    c->diag_t[4] = now_ns() - sw.t0;
+    // A window holding k = 0 starts with the k = 0 kernel (search_ctrl.hip) on the second
+    // stream, beside the first md5 launch: launch 0 of the search, with a completion record
+    // of its own that holds its own first hit only.  It is queued right after the first md5
+    // launch (or alone, when the window holds no other k): that launch is the longer one.
+    hipError_t e = hipSuccess;
     StartK0 k0{};
-    LaunchSlot *k0slot = nullptr;
+    bool k0_pending = false;
+    auto queue_k0 = [&]() -> int {
+        if (!k0_pending) return 0;
+        k0_pending = false;
+        LaunchSlot &k0slot = c->slots[seq0 % kRing];
+        e = search_k0(k0, c->aux_stream);
+        if (e != hipSuccess) return hip_fail(e, "search_k0");
+        k0slot.in_flight = true;
+        c->diag_t[0] = now_ns() - sw.t0;
+        return 0;
+    };
     if (have && pl.k0) {
-        k0slot = &c->slots[seq0 % kRing];
-        if (harvest(c, *k0slot) < 0) return DPOW_EHIP;
+        LaunchSlot &k0slot = c->slots[seq0 % kRing];
+        if ((rc = retire_slot(c, k0slot)) < 0) return rc;
+        c->diag_t[5] = now_ns() - sw.t0;
         k0.r = (uint32_t)(pl.L.i_end - pl.L.i_begin);
         k0.base_tb = pl.L.base_tb;
         k0.nblk = pl.info.nblk;
@@ -325,37 +350,41 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         k0.snap = c->d_snap + seq0 % kRing;
         memcpy(k0.iv, pl.L.iv, sizeof k0.iv);
         memcpy(k0.T, pl.L.T, sizeof k0.T);
-    }
-    c->reset_done = k0slot ? k0slot->end : c->reset_ev;
-    hipError_t e = search_start(c->d_ctrl, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot),
-                                node_best < bound ? node_best : bound, k0, c->stream,
-                                k0slot ? k0slot->start : nullptr, c->reset_done);
-    if (e != hipSuccess) return hip_fail(e, "search_start");
-    if (k0slot) {
-        k0slot->pending = true;
-        k0slot->counted = false;
-        k0slot->candidates = k0.r;
-        k0slot->g_end = 1ull << 8;
+        k0_pending = true;
+        k0slot.seq = seq0;
+        k0slot.candidates = k0.r;
+        k0slot.g_end = 1ull << 8;
+        k0slot.stream = c->aux_stream;
         c->seq = seq0 + 1;
         launched = 1;
-        busy_until = now_ns() + kEstFixedNs;
         have = planner.next(pl);
     }
-    // Open the window for dpow_search_bound; closed (and its atomicMin kernels
-    // drained, so none lands on the next search's reset) on every return path.
+    // This search's control block (clean: reset by the previous search's launches, or at
+    // dpow_open); its md5 launches reset the next one.
+    Ctrl *const ctrl = c->d_ctrl + (size_t)c->ctrl_idx * kCtrlStride;
+    Ctrl *const ctrl_next = c->d_ctrl + (size_t)((c->ctrl_idx + 1) % kCtrlRing) * kCtrlStride;
+    bool md5_queued = false;
+    struct CtrlAdvance {  // once an md5 launch is queued, the next search uses the next block
+        dpow_ctx *c;
+        const bool &queued;
+        ~CtrlAdvance() {
+            if (queued) c->ctrl_idx = (c->ctrl_idx + 1) % kCtrlRing;
+        }
+    } ctrl_advance{c, md5_queued};
+    const uint64_t bound0 = node_best < bound ? node_best : bound;
+    // Open the window for dpow_search_bound (the bound word starts at "none" for this
+    // search; stale launches of the previous one may still read it, harmlessly).
     struct BoundWindow {
         dpow_ctx *c;
         BoundWindow(dpow_ctx *cc, uint64_t start) : c(cc) {
             std::lock_guard<std::mutex> g(c->bound_mu);
             c->ext_bound.store(start, std::memory_order_relaxed);
+            __atomic_store_n(bound_word(c), (uint64_t)DPOW_NO_HIT, __ATOMIC_RELEASE);
             c->searching = true;
         }
         ~BoundWindow() {
-            {
-                std::lock_guard<std::mutex> g(c->bound_mu);
-                c->searching = false;
-            }
-            (void)hipStreamSynchronize(c->bound_stream);
+            std::lock_guard<std::mutex> g(c->bound_mu);
+            c->searching = false;
         }
     } bound_window(c, node_best);
 
@@ -382,9 +411,14 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         const int rc = wait_record(c, seq, kNoDeadline, sw);
         if (rc < 0) return rc;
         LaunchSlot &slot = c->slots[seq % kRing];
-        slot.counted = true;
-        consumed = lj + 1;
         const Snap &sn = c->h_snap[seq % kRing];
+        slot.in_flight = false;
+        c->stats.launches++;
+        c->stats.candidates += slot.candidates;
+        if (sn.t_start != 0ull && sn.t_end >= sn.t_start)
+            c->stats.kernel_ms += (double)(sn.t_end - sn.t_start) * kRealtimeNs * 1e-6;
+        if (consumed == 0) c->diag_t[2] = now_ns() - sw.t0;
+        consumed = lj + 1;
         // The watcher may have put the node slot's best into Ctrl::best before this thread
         // saw it: read the slot now (its best only decreases) so ext_bound covers it.
         if (c->node) {
@@ -439,33 +473,42 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         }
         const uint64_t seq = seq0 + li;
         LaunchSlot &slot = c->slots[seq % kRing];
-        if (harvest(c, slot) < 0) return DPOW_EHIP;  // the slot's previous launch
+        if ((rc = retire_slot(c, slot)) < 0) return rc;  // the slot's previous user
+        if (!md5_queued) c->diag_t[6] = now_ns() - sw.t0;
         Launch &L = pl.L;
         // This search's share of the device's resident workgroups (1 / searches in flight on it).
         const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
-        const uint64_t bpc = launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
+        const uint64_t bpc = c->bpc_override ? c->bpc_override : launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
         const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * bpc / share, kClaimCounters);
         uint64_t worker_blocks = 0;
-        rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), &worker_blocks);
+        rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), &worker_blocks,
+                         c->min_chunk_override ? c->min_chunk_override : launch_min_chunk(ntz, L.rbits));
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.poll_wb = c->poll_override ? c->poll_override : launch_poll_wb(ntz, L.rbits);
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
         L.done_target = done_target;
-        L.ctrl = c->d_ctrl;
+        L.ctrl = ctrl;
+        L.ctrl_next = ctrl_next;
+        L.bound0 = bound0;
         L.cancel = c->d_cancel;
         L.stale = c->d_cancel + kStaleWord;
+        L.ext_bound = reinterpret_cast<const unsigned long long *>(c->d_cancel + kBoundWord);
         L.snap = c->d_snap + seq % kRing;
         L.seq = (uint32_t)(seq + 1);
         L.node_best = c->d_node ? reinterpret_cast<const unsigned long long *>(&c->d_node->best) : nullptr;
         L.node_stop = c->d_node ? &c->d_node->stop : nullptr;
         e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L, (uint32_t)(worker_blocks + 1),
-                          c->stream, slot.start, slot.end);
+                          c->stream);
         if (e != hipSuccess) return hip_fail(e, "search_launch");
-        slot.pending = true;
-        slot.counted = false;
+        if (!md5_queued) c->diag_t[1] = now_ns() - sw.t0;
+        md5_queued = true;
+        if (k0_pending && (rc = queue_k0()) < 0) return rc;
+        slot.seq = seq;
+        slot.in_flight = true;
         slot.candidates = L.i_end - L.i_begin;
         slot.g_end = pl.info.k_end << 8;
+        slot.stream = c->stream;
         c->seq = seq + 1;
         ++launched;
         const int64_t t = now_ns();
@@ -473,12 +516,14 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
                      (int64_t)((double)slot.candidates * (double)share / kEstRate * 1e9);
         have = planner.next(pl);
     }
+    if (k0_pending && (rc = queue_k0()) < 0) return rc;  // no md5 launch was queued
     while (status == DPOW_EXHAUSTED && consumed < launched) {  // the window is queued: drain in order
         const int r = consume(consumed);
         if (r < 0) return r;
         status = r;
     }
     if (status == DPOW_BOUNDED) status = DPOW_EXHAUSTED;  // no hit below the (injected) bound
+    c->diag_t[3] = now_ns() - sw.t0;
 
     if (status == DPOW_FOUND) {
         dpow_secret_from_index(best, secret_out, secret_len);
@@ -525,25 +570,33 @@ int dpow_open(int device, dpow_ctx **out) {
     }
     c->cus = (uint32_t)prop.multiProcessorCount;
     if (const char *pw = getenv("DPOW_DIAG_POLL_WB")) c->poll_override = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_BPC")) c->bpc_override = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_MIN_CHUNK")) {
+        const uint32_t v = (uint32_t)std::max(0, atoi(pw));
+        if (v && !(v & (v - 1))) c->min_chunk_override = v;
+    }
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->bound_stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&c->reset_ev, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipMalloc(&c->d_ctrl, sizeof(Ctrl))) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc(&c->d_ctrl, kCtrlRing * kCtrlStride * sizeof(Ctrl))) != hipSuccess ||
         (e = hipMalloc(&c->d_claims, kClaimRing * kClaimSlot * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_snap, kRing * sizeof(Snap), hipHostMallocCoherent | hipHostMallocMapped)) !=
             hipSuccess ||
         (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_snap), c->h_snap, 0)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_cancel, 64, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_cancel, kCancelPage, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_cancel), c->h_cancel, 0)) != hipSuccess) {
         dpow_close(c);
         return hip_fail(e, "dpow_open: allocation");
     }
     memset(c->h_snap, 0, kRing * sizeof(Snap));
-    memset(c->h_cancel, 0, 64);
-    for (LaunchSlot &s : c->slots) {
-        if ((e = hipEventCreate(&s.start)) != hipSuccess || (e = hipEventCreate(&s.end)) != hipSuccess) {
+    memset(c->h_cancel, 0, kCancelPage);
+    *bound_word(c) = DPOW_NO_HIT;
+    {   // clean control blocks and zero claim counters (the launches keep them so)
+        std::vector<Ctrl> ring(kCtrlRing * kCtrlStride, Ctrl{kNoHit, 0u, 0u});
+        if ((e = hipMemcpy(c->d_ctrl, ring.data(), ring.size() * sizeof(Ctrl), hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemset(c->d_claims, 0, kClaimRing * kClaimSlot * sizeof(unsigned long long))) != hipSuccess ||
+            (e = hipDeviceSynchronize()) != hipSuccess) {
             dpow_close(c);
-            return hip_fail(e, "dpow_open: hipEventCreate");
+            return hip_fail(e, "dpow_open: control state");
         }
     }
     *out = c;
@@ -554,20 +607,15 @@ void dpow_close(dpow_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (LaunchSlot &s : c->slots) {
-        if (s.start) (void)hipEventDestroy(s.start);
-        if (s.end) (void)hipEventDestroy(s.end);
-    }
     if (c->d_ctrl) (void)hipFree(c->d_ctrl);
     if (c->d_claims) (void)hipFree(c->d_claims);
     if (c->h_snap) (void)hipHostFree(c->h_snap);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->bound_stream) {
-        (void)hipStreamSynchronize(c->bound_stream);
-        (void)hipStreamDestroy(c->bound_stream);
+    if (c->aux_stream) {
+        (void)hipStreamSynchronize(c->aux_stream);
+        (void)hipStreamDestroy(c->aux_stream);
     }
-    if (c->reset_ev) (void)hipEventDestroy(c->reset_ev);
     for (void *p : c->registered) (void)hipHostUnregister(p);
     delete c;
 }
@@ -586,14 +634,12 @@ int dpow_geometry(dpow_ctx *c, uint32_t *cus, uint32_t *blocks_per_cu, uint32_t 
 
 int dpow_get_stats(dpow_ctx *c, dpow_stats *out) {
     if (!c || !out) return set_error(DPOW_EINVAL, "dpow_get_stats: NULL argument");
-    if (harvest_all(c) < 0) return DPOW_EHIP;
     *out = c->stats;
     return 0;
 }
 
 void dpow_reset_stats(dpow_ctx *c) {
     if (!c) return;
-    (void)harvest_all(c);  // launches queued before the reset stay out of the new counts
     c->stats = dpow_stats{};
 }
 
@@ -732,6 +778,12 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
         ++n;
     }
     return (int)n;
+}
+
+int dpow_diag_search_times(dpow_ctx *c, int64_t out[8]) {
+    if (!c || !out) return set_error(DPOW_EINVAL, "dpow_diag_search_times: NULL argument");
+    for (int i = 0; i < 8; ++i) out[i] = c->diag_t[i];
+    return 0;
 }
 
 uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t worker_bits) {

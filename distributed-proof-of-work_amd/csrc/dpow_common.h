@@ -76,12 +76,18 @@ constexpr uint32_t kClaimCounters = 8;
 constexpr uint32_t kClaimStride = 16;  // unsigned long long units (128 B)
 constexpr uint32_t kClaimSlot = kClaimCounters * kClaimStride;  // one launch's counters
 
-// Device control block (one per context, in HBM).
+// Device control block of one search (a context keeps a ring of kCtrlRing in HBM, each
+// on its own 128-byte line).  A search's launches find theirs clean -- reset by the
+// previous search's launches (Launch::ctrl_next), or at dpow_open -- so a search needs
+// no reset kernel in front of its first launch.
+constexpr unsigned long long kNoHit = 0x7FFFFFFFFFFFFFFFull;  // = DPOW_NO_HIT (include/dpow.h)
 struct Ctrl {
-    unsigned long long best;  // min global index found (DPOW_NO_HIT = none), atomicMin target
+    unsigned long long best;  // min global index found (kNoHit = none), atomicMin target
     uint32_t stop;            // set by the watcher when the host cancel flag is raised
     uint32_t done;            // worker workgroups retired (cumulative within one search)
 };
+constexpr uint32_t kCtrlRing = 4;
+constexpr uint32_t kCtrlStride = 128 / sizeof(Ctrl);  // Ctrl units between ring entries
 
 // Host-visible completion record of one launch (pinned, host-coherent, mapped).
 // The launch's last retiring workgroup writes it: the
@@ -91,7 +97,9 @@ struct Snap {
     unsigned long long best;
     uint32_t stop;
     uint32_t seq;  // launch sequence number + 1 (0 = never written)
+    unsigned long long t_start, t_end;  // s_memrealtime (100 MHz) at the launch's start and at the record
 };
+constexpr double kRealtimeNs = 10.0;  // ns per s_memrealtime tick (100 MHz)
 
 // One launch window.  Passed by value as the kernel argument (kernarg segment,
 // read with scalar loads).
@@ -119,16 +127,22 @@ struct Launch {
     uint64_t n_big;        // claims of `chunk` wave-blocks
     uint64_t n_chunks;     // claims covering n_wblocks (n_big + tail claims)
     uint64_t n_head;       // the claims every wave takes at its start (2 per wave): hashed at raised priority
+    uint64_t n_static;     // claims [0, n_static) are handed out by wave index, not by a counter: worker
+                           //  wave w's first claim is w (the "_ls" kernels only; 0 for every other launch)
     uint32_t poll_wb;      // wave-blocks per group: a wave reads Ctrl::best / Ctrl::stop once per group
     uint32_t pad0;
     unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
-    Ctrl *ctrl;
+    Ctrl *ctrl;              // this search's control block (clean at its first launch)
+    Ctrl *ctrl_next;         // the next search's: reset by this launch's last workgroup
     const uint32_t *cancel;  // device-visible alias of the pinned host cancel flag
     const uint32_t *stale;   // pinned: launches with seq <= *stale (mod 2^32) belong to a cancelled search
+    const unsigned long long *ext_bound;  // pinned: the bound dpow_search_bound injected (the watcher relays it)
     Snap *snap;              // device alias of this launch's pinned completion record
     uint32_t seq;            // value the last workgroup writes to snap->seq
     uint32_t pad1;
+    unsigned long long bound0;  // the search's bound at its start (the caller's, the node slot's):
+                                //  a wave starts from min(Ctrl::best, bound0)
     // Node slot (dpow_node_attach; null when none): device aliases of the slot's best and
     // stop in the node's shared host memory, polled by the watcher -- another rank's hit
     // lowers Ctrl::best, a raised stop stops the launch.

@@ -3,16 +3,15 @@
 
 namespace dpow {
 
-hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream,
-                         hipEvent_t start, hipEvent_t stop) {
+hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream) {
     if (!variant_exists(nblk, w0, sh)) return hipErrorInvalidValue;
     if (L.seg0 == kLsegBase) {
         if (sh != 0) return hipErrorInvalidValue;
-        return nblk == 1 ? variant_launch_1_0_ls(w0, L, grid, stream, start, stop)
-                         : variant_launch_2_0_ls(w0, L, grid, stream, start, stop);
+        return nblk == 1 ? variant_launch_1_0_ls(w0, L, grid, stream)
+                         : variant_launch_2_0_ls(w0, L, grid, stream);
     }
 #define DPOW_CASE(n, s) \
-    if (nblk == n && sh == s) return variant_launch_##n##_##s(w0, L, grid, stream, start, stop);
+    if (nblk == n && sh == s) return variant_launch_##n##_##s(w0, L, grid, stream);
     DPOW_CASE(1, 0) DPOW_CASE(1, 1) DPOW_CASE(1, 2) DPOW_CASE(1, 3)
     DPOW_CASE(2, 0) DPOW_CASE(2, 1) DPOW_CASE(2, 2) DPOW_CASE(2, 3)
 #undef DPOW_CASE

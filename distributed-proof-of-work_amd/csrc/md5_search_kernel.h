@@ -96,6 +96,15 @@ namespace DPOW_KNS {
 #ifndef DPOW_CLAIM_AHEAD
 #define DPOW_CLAIM_AHEAD 1
 #endif
+// Static first claims (the "_ls" kernels: the short launches below k = 2^24 that the
+// time-to-secret path runs): worker wave w's first claim is chunk w, so a wave starts
+// hashing without waiting for a contended counter -- at 4 workgroups per CU the start-up
+// burst of 8k claim atomics on 8 counters held the median wave 5 us and the slowest 10 us
+// before its first wave-block (tools/wave_trace_tts.py).  Its claim-ahead atomic then
+// hides behind that first chunk.  The counters hand out chunks from Launch::n_static on.
+#ifndef DPOW_STATIC_FIRST
+#define DPOW_STATIC_FIRST DPOW_VLS
+#endif
 #ifndef DPOW_CLAIM_DEFER
 #define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch;
                             // one final block only, search_body kDeferClaims)
@@ -657,13 +666,26 @@ DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_
 // not in the watcher: either inlined form makes the register allocator spill
 // SGPRs inside the hash loop (tools/isa_loop.py: 7-11 v_readlane per
 // wave-block, -3.5 % throughput).
-__device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim) {
-    // Every workgroup has left its claim loop: recycle the counter slot.
+//
+// It also resets the next search's control block (ctrl_next): every launch of this search
+// runs before any of the next one's (stream order), so the next search needs no reset
+// kernel in front of its first launch.
+__device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim,
+                                                  Ctrl *ctrl_next) {
+    // Every workgroup has left its claim loop: recycle the counter slot (claim[1]: the
+    // launch's start time, written by the watcher).
+    const unsigned long long t_start = __hip_atomic_load(&claim[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint32_t x = 0; x < kClaimCounters; ++x) claim[x * kClaimStride] = 0ull;
+    claim[1] = 0ull;
+    ctrl_next->best = kNoHit;
+    ctrl_next->stop = 0u;
+    ctrl_next->done = 0u;
     const unsigned long long best = __hip_atomic_load(&ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t stop = __hip_atomic_load(&ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&snap->best, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&snap->stop, stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&snap->t_start, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&snap->t_end, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&snap->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -679,15 +701,28 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 // group -- and a raised node stop stops the launch.  The host injecting the same best
 // through a kernel on a second stream took 50-160 us to start that kernel beside the
 // running grid (profiles/r03_stop_latency.json).
+//
+// The bound injected by dpow_search_bound (a pinned host word) is relayed the same way.
+//
+// It also stamps the launch's start (s_memrealtime into the claim slot's spare word): the
+// watcher workgroup is dispatched first, and the kernel time in the completion record
+// replaces per-launch HIP timing events, whose profiling packets cost the host ~4.5 us per
+// launch on the time-to-secret path (tools/small_search_probe.py, DPOW_DIAG_NO_EVENTS).
 DPOW_DEV void watcher(const Launch &L) {
     if (threadIdx.x != 0) return;
-    unsigned long long node_seen = ~0ull;
+    __hip_atomic_store(&L.claim[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long node_seen = ~0ull, bound_seen = L.bound0;
     for (;;) {
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (done >= L.done_target) return;
         const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         bool stop = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
                     (int32_t)(stale - L.seq) >= 0;
+        const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (eb < bound_seen) {
+            bound_seen = eb;
+            __hip_atomic_fetch_min(&L.ctrl->best, eb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (L.node_best) {
             const unsigned long long nb = __hip_atomic_load(L.node_best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (nb < node_seen) {
@@ -724,14 +759,15 @@ DPOW_DEV unsigned long long claim_issue(unsigned long long *ctr, uint32_t lane) 
     return v;
 }
 
-DPOW_DEV uint64_t claim_take(unsigned long long v, uint32_t x) {
+// base: the first counter-handed claim (Launch::n_static with static first claims, else 0).
+DPOW_DEV uint64_t claim_take(unsigned long long v, uint32_t x, uint64_t base) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (((uint64_t)hi << 32) | lo) * kClaimCounters + x;
+    return (((uint64_t)hi << 32) | lo) * kClaimCounters + x + base;
 }
 
-DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t x, uint32_t lane) {
-    return claim_take(claim_issue<false>(ctr, lane), x);
+DPOW_DEV uint64_t claim_next(unsigned long long *ctr, uint32_t x, uint32_t lane, uint64_t base) {
+    return claim_take(claim_issue<false>(ctr, lane), x, base);
 }
 
 DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
@@ -849,6 +885,7 @@ DPOW_DEV void search_body(const Launch &L) {
     uint32_t lov = loff;
 
     unsigned long long best = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    best = best < L.bound0 ? best : L.bound0;
     uint32_t stop = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // Waves claim chunks of L.chunk consecutive wave-blocks from their XCD's
@@ -879,7 +916,15 @@ DPOW_DEV void search_body(const Launch &L) {
     constexpr bool kDeferClaims = DPOW_CLAIM_DEFER && NBLK == 1;
     uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
-    uint64_t claim = skip ? L.n_chunks : claim_next(L.claim + x * kClaimStride, x, lane);
+#if DPOW_STATIC_FIRST
+    const uint64_t cbase = L.n_static;
+    const uint32_t wave_id = __builtin_amdgcn_readfirstlane((blockIdx.x - 1u) * (kBlockThreads / 64) + threadIdx.x / 64u);
+    uint64_t claim = skip ? L.n_chunks
+                          : (wave_id < cbase ? (uint64_t)wave_id : claim_next(L.claim + x * kClaimStride, x, lane, cbase));
+#else
+    constexpr uint64_t cbase = 0;
+    uint64_t claim = skip ? L.n_chunks : claim_next(L.claim + x * kClaimStride, x, lane, cbase);
+#endif
 #if DPOW_WAVE_TRACE
     t_first = __builtin_amdgcn_s_memrealtime() + (claim & 0);
 #endif
@@ -894,8 +939,9 @@ DPOW_DEV void search_body(const Launch &L) {
             x = (x + 1u) % kClaimCounters;
             const unsigned long long seen =
                 __hip_atomic_load(L.claim + x * kClaimStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            claim = seen * kClaimCounters + x < L.n_chunks ? claim_next(L.claim + x * kClaimStride, x, lane)
-                                                             : L.n_chunks;
+            claim = seen * kClaimCounters + x + cbase < L.n_chunks
+                        ? claim_next(L.claim + x * kClaimStride, x, lane, cbase)
+                        : L.n_chunks;
             continue;
         }
 #else
@@ -907,7 +953,7 @@ DPOW_DEV void search_body(const Launch &L) {
         unsigned long long next_v = 0;
         uint64_t next = 0;
         if constexpr (kDeferClaims) next_v = claim_issue<true>(L.claim + x * kClaimStride, lane);
-        else next = claim_next(L.claim + x * kClaimStride, x, lane);
+        else next = claim_next(L.claim + x * kClaimStride, x, lane, cbase);
 #endif
         // Claims [0, n_big) are `chunk` wave-blocks, the rest `chunk_tail`: the
         // launch ends on small claims, so its waves run dry within a few
@@ -1003,11 +1049,11 @@ DPOW_DEV void search_body(const Launch &L) {
         stop = stop_next;
 #endif
 #if DPOW_CLAIM_AHEAD
-        if constexpr (kDeferClaims) claim = claim_take(next_v, x);
+        if constexpr (kDeferClaims) claim = claim_take(next_v, x, cbase);
         else claim = next;
 #else
         if (stop != 0u) break;
-        claim = claim_next(L.claim + x * kClaimStride, x, lane);
+        claim = claim_next(L.claim + x * kClaimStride, x, lane, cbase);
 #endif
     }
     // Retirement is counted per workgroup (a quarter of the atomics on the
@@ -1038,7 +1084,7 @@ DPOW_DEV void search_body(const Launch &L) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim);
+        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, L.ctrl_next);
     }
 }
 

@@ -59,10 +59,10 @@ KernelFn pick(int w0, bool eq) {
 #define DPOW_NAME(a, b, c) DPOW_NAME2(a, b, c, DPOW_SFX)
 
 hipError_t DPOW_NAME(variant_launch_, DPOW_VNBLK, DPOW_VSH)(int w0, const Launch &L, uint32_t grid,
-                                                           hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
+                                                           hipStream_t stream) {
     KernelFn fn = pick(w0, use_d_equality(DPOW_VNBLK, L.ntz));
     if (!fn) return hipErrorInvalidValue;
-    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kBlockThreads), 0, stream, start, stop, 0, L);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlockThreads), 0, stream, L);
     return hipGetLastError();
 }
 
@@ -75,9 +75,14 @@ hipError_t DPOW_NAME(variant_occupancy_, DPOW_VNBLK, DPOW_VSH)(int w0, int *bloc
 
 }  // namespace dpow
 
-#if DPOW_WAVE_TRACE && DPOW_VNBLK == 1 && DPOW_VSH == 0 && !DPOW_VLS
-// Diagnostic builds only: the per-wave trace of the last one-block, SH = 0 launch.
+#if DPOW_WAVE_TRACE && DPOW_VNBLK == 1 && DPOW_VSH == 0
+// Diagnostic builds only: the per-wave trace of the last one-block, SH = 0 launch
+// (dpow_diag_wave_trace_ls: of the last chunk-length-spanning one, below k = 2^24).
+#if DPOW_VLS
+extern "C" int dpow_diag_wave_trace_ls(unsigned long long *out, size_t n) {
+#else
 extern "C" int dpow_diag_wave_trace(unsigned long long *out, size_t n) {
+#endif
     if (n > dpow::DPOW_KNS::kTraceWaves * 4) n = dpow::DPOW_KNS::kTraceWaves * 4;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(dpow::DPOW_KNS::g_wave_trace), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
                ? 0

@@ -8,8 +8,7 @@
 namespace dpow {
 
 #define DPOW_DECL_VARIANT(n, s)                                                                  \
-    hipError_t variant_launch_##n##_##s(int w0, const Launch &L, uint32_t grid, hipStream_t st, \
-                                        hipEvent_t start, hipEvent_t stop);                      \
+    hipError_t variant_launch_##n##_##s(int w0, const Launch &L, uint32_t grid, hipStream_t st); \
     hipError_t variant_occupancy_##n##_##s(int w0, int *blocks_per_cu);
 DPOW_DECL_VARIANT(1, 0)
 DPOW_DECL_VARIANT(1, 1)
@@ -31,23 +30,16 @@ inline bool variant_exists(int nblk, int w0, int sh) {
     return false;
 }
 
-// start / stop (may be null): timing events recorded by the kernel's own dispatch
-// packet (hipExtLaunchKernel), not as separate marker packets between launches.
 // Launches whose template is chunk length 0's (L.seg0 == kLsegBase: SH = 0 below k = 2^24)
-// run the "_ls" kernels.
-hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream,
-                         hipEvent_t start, hipEvent_t stop);
+// run the "_ls" kernels.  (No timing events: the kernel stamps its start and end into its
+// completion record.)
+hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream);
 hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu);
 
-// Lower a running search's Ctrl::best to an external bound (search_ctrl.hip).
-hipError_t search_bound(Ctrl *ctrl, unsigned long long g, hipStream_t stream);
-
-// Per-search reset of the control block and claim counters (search_ctrl.hip).
-// The search's start kernel (search_ctrl.hip): resets the control block to `bound` and the
-// claim counters, and -- when k0.r > 0 -- hashes the k = 0 candidates (msg = nonce ||
-// threadByte, R of them), their first hit to Ctrl::best, then writes k0.snap's record.
+// The k = 0 kernel (search_ctrl.hip): hashes the k = 0 candidates (msg = nonce ||
+// threadByte, R of them) and writes k0.snap's record with their first hit.
 struct StartK0 {
-    uint32_t r;        // threadBytes of the partition (R), 0 = no k = 0 work
+    uint32_t r;        // threadBytes of the partition (R)
     uint32_t base_tb;  // uint8(worker_byte << R_bits)
     uint32_t nblk;     // final blocks of the k = 0 message
     uint32_t p;        // byte offset of the threadByte in them
@@ -57,8 +49,6 @@ struct StartK0 {
     uint32_t iv[4];    // chaining value entering the final blocks
     uint32_t T[32];    // their words, threadByte zeroed (plan.cpp build_template)
 };
-// start / stop (may be null) are recorded by the kernel's own dispatch.
-hipError_t search_start(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
-                        const StartK0 &k0, hipStream_t stream, hipEvent_t start, hipEvent_t stop);
+hipError_t search_k0(const StartK0 &k0, hipStream_t stream);
 
 }  // namespace dpow

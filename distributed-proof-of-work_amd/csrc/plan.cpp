@@ -233,7 +233,8 @@ uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits) {
     return ((1ull << (4 * ntz)) << rbits) >> 8;
 }
 
-int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks_out) {
+int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks_out,
+                uint64_t min_chunk) {
     Launch &L = pl.L;
     constexpr uint64_t wpb = kBlockThreads / 64;
     // Chunk: >= kClaimsPerWave claims per wave of the largest grid the launch gets, over
@@ -249,7 +250,7 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
     uint64_t span_wb = L.n_wblocks;
     if (expect / (uint64_t)kWaveBlock < span_wb) span_wb = expect / (uint64_t)kWaveBlock;
     uint64_t chunk = span_wb / (worker_blocks * wpb * kClaimsPerWave);
-    if (chunk < kMinChunk) chunk = kMinChunk;
+    if (chunk < min_chunk) chunk = min_chunk;
     if (chunk > kMaxChunk) chunk = kMaxChunk;
     if ((DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) || L.lspan) {
         // The launch spans 2^24-k segments: a power-of-two chunk and wave-blocks
@@ -289,13 +290,26 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
     L.n_big = n_big;
     L.n_chunks = n_chunks;
     L.n_head = 2 * worker_blocks * wpb;
+    // Static first claims (md5_search_kernel.h DPOW_STATIC_FIRST): the "_ls" kernels (the
+    // chunk-length-0 template, L.seg0 == kLsegBase) hand claim w to worker wave w.  Every
+    // counter that holds a claim beyond them still has a workgroup (checked above on
+    // n_chunks, which bounds the counters' share too).
+    L.n_static = DPOW_STATIC_FIRST_HOST && L.seg0 == kLsegBase && !pl.k0
+                     ? (n_chunks < worker_blocks * wpb ? n_chunks : worker_blocks * wpb)
+                     : 0;
     *worker_blocks_out = worker_blocks;
     return 0;
 }
 
 uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits) {
     const uint32_t slow = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 16;
-    return expected_first_hit(ntz, rbits) <= kFastPollCands ? kFastPollWb : slow;
+    const uint64_t expect = expected_first_hit(ntz, rbits);
+    if (DPOW_SMALL_GRIDS && expect <= kTinyExpect) return 1;
+    return expect <= kFastPollCands ? kFastPollWb : slow;
+}
+
+uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits) {
+    return DPOW_SMALL_GRIDS && expected_first_hit(ntz, rbits) <= kTinyExpect ? kTinyChunk : kMinChunk;
 }
 
 uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits) {
@@ -303,6 +317,7 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits)
     // Candidates of this partition expected before its first hit: 16^N R / 256.
     const uint64_t expect = expected_first_hit(ntz, rbits);
     const uint64_t eff = candidates < expect ? candidates : expect;
+    if (eff <= kTinyExpect) return kMaxBlocksPerCu < 2 ? kMaxBlocksPerCu : 2;
     if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
     if (eff <= (1ull << 24)) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
 #else

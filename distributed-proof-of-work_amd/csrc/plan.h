@@ -30,6 +30,10 @@ bool lspan_layout(size_t nonce_len, uint32_t rbits, uint32_t ntz);
 #ifndef DPOW_START_K0
 #define DPOW_START_K0 1  // k = 0 hashed by the search's start kernel (A/B switch)
 #endif
+#ifndef DPOW_STATIC_FIRST_HOST
+#define DPOW_STATIC_FIRST_HOST 1  // static first claims in the "_ls" kernels (A/B switch; the kernels'
+                                  // DPOW_STATIC_FIRST must match: both read Launch::n_static)
+#endif
 uint32_t remainder_bits(uint32_t worker_bits);
 uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits);
 
@@ -85,7 +89,9 @@ static_assert((kMinChunk & (kMinChunk - 1)) == 0 && (kMaxChunk & (kMaxChunk - 1)
               "chunk bounds are powers of two (segment alignment)");
 // expect: candidates of the launch expected before its first hit (expected_first_hit;
 // ~0 = none): chunks are sized so that >= kClaimsPerWave claims per wave come before it.
-int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks);
+// min_chunk: a power of two (diagnostic override of kMinChunk, dpow_api.cpp).
+int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks,
+                uint64_t min_chunk = kMinChunk);
 // Mean number of a partition's candidates before its first hit at N trailing zeros.
 uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits);
 
@@ -104,6 +110,17 @@ uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits);
 constexpr uint32_t kFastPollWb = DPOW_FAST_POLL_WB;
 constexpr uint64_t kFastPollCands = 1ull << 30;
 uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
+// Tiny searches -- a first hit expected within kTinyExpect candidates of the partition (N <= 5
+// on one GPU, N = 6 on a rank of an 8-GPU node): 2 workgroups per CU, claims of >= 2
+// wave-blocks, a poll of Ctrl::best after every wave-block.  There the launch's fixed cost
+// -- the waves' first chunks, the drain behind the hit -- outweighs its hashing: each wave
+// of a lightly loaded SIMD finishes a wave-block sooner.  Measured over the BASELINE cases
+// and 24 fresh nonces each (tools/small_search_probe.py, profiles/r03_small_probe.json):
+// [5,6,7,8]/5 0.040 -> 0.025 ms, fresh N = 5 0.044 -> 0.035 ms, an 8-GPU rank's
+// [1,2,3,4]/6 0.043 -> 0.026 ms.
+constexpr uint64_t kTinyExpect = 1ull << 21;
+constexpr uint64_t kTinyChunk = 2;
+uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits);
 
 // Worker workgroups per CU for one launch (before the device share).  The full
 // persistent grid (kMaxBlocksPerCu = 6) has the highest rate, but a launch that is

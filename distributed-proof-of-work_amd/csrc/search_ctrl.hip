@@ -1,14 +1,14 @@
-// search_ctrl.hip -- the start kernel of a search: resets a context's device control
-// state and hashes the chunk of zero bytes (k = 0).
+// search_ctrl.hip -- the k = 0 kernel of a search window that starts at k = 0.
 //
-// One small kernel on the context stream replaces a host->device copy of the
-// control block and a memset of the claim counters (each an SDMA round trip of
-// tens of microseconds on the time-to-secret path).  k = 0 is the one chunk whose
-// message layout (msg = nonce || threadByte, the 0x80 pad right behind it) differs
-// from every other chunk's within a wave: a wave of an md5 launch holds 64 / R
-// consecutive k, so for R <= 64 it would mix k = 0 and k = 1.  Its R <= 256 candidates
-// are hashed here instead, one per thread, before the search's first md5 launch
-// (which then starts at k = 1 and may span chunk lengths 1..3: plan.cpp).
+// k = 0 is the one chunk whose message layout (msg = nonce || threadByte, the 0x80 pad
+// right behind it) differs from every other chunk's within a wave: a wave of an md5
+// launch holds 64 / R consecutive k, so for R <= 64 it would mix k = 0 and k = 1.  Its
+// R <= 256 candidates are hashed here instead, one per thread, on the context's second
+// stream beside the search's first md5 launch (which starts at k = 1 and may span chunk
+// lengths 1..3: plan.cpp).  (Round 3 start: this kernel also reset the control block and
+// claim counters, in front of the first md5 launch on the same stream -- 15 us on every
+// search's time-to-secret path; the launches now reset the next search's control block
+// themselves, md5_search_kernel.h publish().)
 #include <hip/hip_runtime.h>
 
 #include "dpow_common.h"
@@ -42,20 +42,16 @@ __device__ void md5_block(uint32_t st[4], const uint32_t M[16]) {
     st[3] += d;
 }
 
-// Control block and claim counters [0, n_claims); then the k = 0 candidates, one per
-// thread (worker.go:318-356 for chunk_0 = []: msg = nonce || threadByte).
-__global__ void __launch_bounds__(kBlockThreads) search_start_kernel(Ctrl *ctrl, unsigned long long *claims,
-                                                                     uint32_t n_claims, unsigned long long bound,
-                                                                     const StartK0 k0) {
-    if (threadIdx.x == 0) {
-        ctrl->best = bound;
-        ctrl->stop = 0u;
-        ctrl->done = 0u;
-    }
-    for (uint32_t i = threadIdx.x; i < n_claims; i += kBlockThreads) claims[i] = 0ull;
-    if (k0.r == 0u) return;
-    __threadfence();
-    __syncthreads();  // Ctrl::best holds the bound before any hit is min'ed into it
+// The k = 0 candidates, one per thread (worker.go:318-356 for chunk_0 = []: msg = nonce ||
+// threadByte), and the kernel's own completion record: {its first hit, or kNoHit}.  It
+// touches no control block: it runs on the context's second stream beside the search's
+// first md5 launch, and the host consumes its record first (the lowest indices of the
+// window), so a hit here ends the search and the md5 launches are stopped as stale.
+__global__ void __launch_bounds__(kBlockThreads) search_k0_kernel(const StartK0 k0) {
+    __shared__ unsigned long long hit;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) hit = kNoHit;
+    __syncthreads();
     if (threadIdx.x < k0.r) {
         const uint32_t tb = k0.base_tb | threadIdx.x;
         uint32_t st[4] = {k0.iv[0], k0.iv[1], k0.iv[2], k0.iv[3]};
@@ -71,38 +67,23 @@ __global__ void __launch_bounds__(kBlockThreads) search_start_kernel(Ctrl *ctrl,
             }
             md5_block(st, M);
         }
-        if (trailing_zero_nibbles(st[0], st[1], st[2], st[3]) >= k0.ntz) {
-            // g = 0 * 256 + threadByte; a returning atomic, consumed: performed before the barrier
-            const unsigned long long prev =
-                __hip_atomic_fetch_min(&ctrl->best, (unsigned long long)tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("; dpow: k0 atomicMin performed (%0)" ::"v"(prev));
-        }
+        // g = 0 * 256 + threadByte
+        if (trailing_zero_nibbles(st[0], st[1], st[2], st[3]) >= k0.ntz) atomicMin(&hit, (unsigned long long)tb);
     }
-    __threadfence();
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned long long best = __hip_atomic_load(&ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&k0.snap->best, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&k0.snap->best, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&k0.snap->stop, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&k0.snap->t_start, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&k0.snap->t_end, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&k0.snap->seq, k0.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
-// Lower Ctrl::best to an external bound (dpow_search_bound) while a search runs:
-// its waves stop claiming work at or above it at their next group.
-__global__ void search_bound_kernel(Ctrl *ctrl, unsigned long long g) {
-    if (threadIdx.x == 0) __hip_atomic_fetch_min(&ctrl->best, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 }  // namespace
 
-hipError_t search_bound(Ctrl *ctrl, unsigned long long g, hipStream_t stream) {
-    hipLaunchKernelGGL(search_bound_kernel, dim3(1), dim3(64), 0, stream, ctrl, g);
-    return hipGetLastError();
-}
-
-hipError_t search_start(Ctrl *ctrl, unsigned long long *claims, uint32_t n_claims, unsigned long long bound,
-                        const StartK0 &k0, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
-    hipExtLaunchKernelGGL(search_start_kernel, dim3(1), dim3(kBlockThreads), 0, stream, start, stop, 0, ctrl, claims,
-                          n_claims, bound, k0);
+hipError_t search_k0(const StartK0 &k0, hipStream_t stream) {
+    hipLaunchKernelGGL(search_k0_kernel, dim3(1), dim3(kBlockThreads), 0, stream, k0);
     return hipGetLastError();
 }
 

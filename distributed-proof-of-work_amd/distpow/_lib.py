@@ -183,6 +183,7 @@ def lib():
         "dpow_diag_dword_test": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64,
                                                 ctypes.c_uint32, ctypes.c_uint32]),
         "dpow_diag_blocks_per_cu": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
+        "dpow_diag_search_times": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "dpow_worker_new": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
         "dpow_worker_free": (None, [vp]),
         "dpow_worker_mine": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,

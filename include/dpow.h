@@ -184,9 +184,10 @@ int dpow_plan_candidate(const uint8_t *nonce, size_t nonce_len, uint32_t worker_
  * ------------------------------------------------------------------------- */
 typedef struct dpow_stats {
     uint64_t searches;     /* dpow_search calls */
-    uint64_t launches;     /* kernel launches */
-    uint64_t candidates;   /* candidates covered by the launched windows */
-    double kernel_ms;      /* sum of per-launch HIP-event durations on the ctx stream */
+    uint64_t launches;     /* kernel launches whose completion record a search consumed */
+    uint64_t candidates;   /* candidates covered by those launches' windows */
+    double kernel_ms;      /* sum of their durations, as each launch stamps them into its
+                              completion record (s_memrealtime at its start and at the record) */
 } dpow_stats;
 int dpow_get_stats(dpow_ctx *ctx, dpow_stats *out);
 void dpow_reset_stats(dpow_ctx *ctx);

@@ -76,6 +76,16 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
  * first hit expected within that many (16^ntz R / 256) -- then 4, or 3 at 2^22. */
 uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t worker_bits);
 
+/* Host timeline of the context's last dpow_search call, ns from its start (-1: did not
+ * happen): [0] the k = 0 kernel queued, [1] the first md5 launch queued, [2] the first
+ * completion record seen, [3] the search done (before the host MD5 re-verification),
+ * [4] the first launch planned, [5] the k = 0 kernel's record slot retired, [6] the
+ * first md5 launch's record slot retired, [7] unused.
+ * Environment overrides read at dpow_open (A/B runs only): DPOW_DIAG_POLL_WB (wave-blocks
+ * per poll group), DPOW_DIAG_BPC (worker workgroups per CU), DPOW_DIAG_MIN_CHUNK (minimum
+ * wave-blocks per claim, a power of two).  Returns 0, or < 0 on error. */
+int dpow_diag_search_times(struct dpow_ctx *ctx, int64_t out[8]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,12 +20,13 @@ with distpow.Miner(0) as m:
     for nonce, n in cases:
         for rep in range(3):
             torch.cuda.synchronize()
-            t0 = time.perf_counter_ns()
             m.reset_stats()
+            t0 = time.perf_counter_ns()
             r = m.mine(nonce, n)
             t1 = time.perf_counter_ns()
             st = m.stats()
             out.append({"case": f"{bytes(nonce).hex()}/{n}", "rep": rep, "ms": (t1 - t0) / 1e6,
+                        "t0_ns": t0, "t1_ns": t1,
                         "g": r.global_idx, "launches": st.launches, "kernel_ms": st.kernel_ms,
                         "candidates": st.candidates})
             time.sleep(0.01)

@@ -178,8 +178,9 @@ def main():
     kernel_ghs = st.candidates / (st.kernel_ms * 1e-3) / 1e9
 
     # time-to-secret for the BASELINE configs (deterministic answers; node-wide when world > 1):
-    # search_ms = the search call (what a worker reports), ms = bracketed by barrier + device
-    # synchronize (it also waits out launches still queued behind the hit)
+    # search_ms = the search call (what a worker reports), ms = up to the device synchronize
+    # after it (it also waits out launches still queued behind the hit), and at N > 1 the
+    # barrier after it (the slowest rank)
     tts = {}
     extra = {}
     ttsk = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8),
@@ -202,7 +203,10 @@ def main():
                                       bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
                                       device=dev, tick_group=tick_group)
             search_runs.append((time.perf_counter() - t1) * 1e3)
-            barrier()
+            if world > 1:
+                barrier()
+            else:  # one rank: the device drained (launches still queued behind the hit retire)
+                torch.cuda.synchronize()
             runs.append((time.perf_counter() - t1) * 1e3)
             assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
         tts[f"{bytes(nonce).hex()}/{n}"] = {"ms": round(sorted(runs)[len(runs) // 2], 3),
@@ -328,9 +332,10 @@ def collective_probe(miner, rank, world, dev, board, backend, reps=200):
     """node_mine's batch boundary on this node's process group (RCCL with the nccl backend):
     median us of [pinned host -> device copy, all-reduce MIN of 3 int64, device -> host
     copy, stream synchronize] -- the per-batch cost c the expected-time batch of
-    node.auto_batch_candidates assumes -- and of one whole node_mine batch over a window
-    of 2^16 candidates per rank (the search call plus the boundary), and node_mine's
-    time-to-secret for two BASELINE cases over this group."""
+    node.auto_batch_candidates assumes -- and, with a shared node board, of the node vote
+    that replaces it there (NodeBoard.vote, all ranks on one host); of one whole node_mine
+    batch over a window of 2^16 candidates per rank (the search call plus the boundary),
+    and node_mine's time-to-secret for two BASELINE cases over this group."""
     on_gpu = dev.type == "cuda"
     buf = torch.zeros(3, dtype=torch.int64, device=dev)
     hbuf = torch.zeros(3, dtype=torch.int64, pin_memory=on_gpu)
@@ -348,6 +353,15 @@ def collective_probe(miner, rank, world, dev, board, backend, reps=200):
         _ = hbuf.tolist()
         if i >= 10:
             lat.append((time.perf_counter() - t) * 1e6)
+    # the node vote (a shared board: every rank on one host), node_mine's boundary there
+    vote = []
+    if board is not None and board.shared:
+        for i in range(reps + 10):
+            dist.barrier()
+            t = time.perf_counter()
+            assert board.vote([i, 1, 1]) == [i, 1, 1]
+            if i >= 10:
+                vote.append((time.perf_counter() - t) * 1e6)
     wb, wbits = partition_of_rank(rank, world)
     R = 1 << (8 - wbits)
     search = lambda *a: miner.search(*a[:6], bound=a[6])  # noqa: E731
@@ -376,6 +390,8 @@ def collective_probe(miner, rank, world, dev, board, backend, reps=200):
     med = lambda v: round(sorted(v)[len(v) // 2], 1)  # noqa: E731
     return {"backend": backend, "world": world,
             "batch_boundary_us": {"median": med(lat), "p90": round(sorted(lat)[int(len(lat) * 0.9)], 1)},
+            "node_vote_us": ({"median": med(vote), "p90": round(sorted(vote)[int(len(vote) * 0.9)], 1)}
+                             if vote else None),
             "batch_2p16_candidates_us": {"median": med(batch), "p90": round(sorted(batch)[int(len(batch) * 0.9)], 1)},
             "node_mine": tts}
 

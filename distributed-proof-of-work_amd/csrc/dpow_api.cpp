@@ -22,9 +22,11 @@
 #include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dpow.h"
+#include "../../include/dpow_worker.h"
 #include "dpow_common.h"
 #include "md5_host.h"
 #include "md5_variants.h"
@@ -188,6 +190,7 @@ struct dpow_ctx {
     uint32_t poll_override = 0;  // DPOW_DIAG_POLL_WB (A/B runs): wave-blocks per poll group for every launch
     uint32_t bpc_override = 0;   // DPOW_DIAG_BPC: worker workgroups per CU for every launch
     uint32_t min_chunk_override = 0;  // DPOW_DIAG_MIN_CHUNK: minimum wave-blocks per claim (a power of two)
+    uint32_t cpw_override = 0;   // DPOW_DIAG_CPW: big claims per wave (chunk sizing)
     int64_t diag_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // the last search's host timeline (dpow_diag_search_times)
 };
 
@@ -482,7 +485,8 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * bpc / share, kClaimCounters);
         uint64_t worker_blocks = 0;
         rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), &worker_blocks,
-                         c->min_chunk_override ? c->min_chunk_override : launch_min_chunk(ntz, L.rbits));
+                         c->min_chunk_override ? c->min_chunk_override : launch_min_chunk(ntz, L.rbits),
+                         c->cpw_override ? c->cpw_override : kClaimsPerWave);
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.poll_wb = c->poll_override ? c->poll_override : launch_poll_wb(ntz, L.rbits);
@@ -571,6 +575,7 @@ int dpow_open(int device, dpow_ctx **out) {
     c->cus = (uint32_t)prop.multiProcessorCount;
     if (const char *pw = getenv("DPOW_DIAG_POLL_WB")) c->poll_override = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_BPC")) c->bpc_override = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_CPW")) c->cpw_override = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_MIN_CHUNK")) {
         const uint32_t v = (uint32_t)std::max(0, atoi(pw));
         if (v && !(v & (v - 1))) c->min_chunk_override = v;
@@ -687,6 +692,58 @@ void dpow_node_post(dpow_node_slot *slot, uint64_t global_idx) {
     while (global_idx < cur &&
            !__atomic_compare_exchange_n(&slot->best, &cur, global_idx, true, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED)) {
     }
+}
+
+int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, uint64_t epoch, const int64_t in[3],
+                   int64_t out[3], int64_t timeout_ns) {
+    if (!votes || !in || !out || world == 0 || rank >= world || epoch == 0)
+        return set_error(DPOW_EINVAL, "dpow_node_vote: bad argument");
+    dpow_node_vote_entry &mine = votes[2 * rank + (epoch & 1)];
+    for (int i = 0; i < 3; ++i) __atomic_store_n(&mine.v[i], in[i], __ATOMIC_RELAXED);
+    __atomic_store_n(&mine.epoch, epoch, __ATOMIC_RELEASE);
+    int64_t acc[3] = {in[0], in[1], in[2]};
+    const int64_t t0 = now_ns();
+    for (uint32_t r = 0; r < world; ++r) {
+        if (r == rank) continue;
+        const dpow_node_vote_entry &e = votes[2 * r + (epoch & 1)];
+        for (uint64_t it = 0; __atomic_load_n(&e.epoch, __ATOMIC_ACQUIRE) != epoch; ++it) {
+            if (it < 4096) {
+                __builtin_ia32_pause();
+                continue;
+            }
+            if (now_ns() - t0 > timeout_ns)
+                return set_error(DPOW_EPROTO, "dpow_node_vote: rank " + std::to_string(r) + " did not vote at epoch " +
+                                                  std::to_string(epoch));
+            const struct timespec d = {0, 2000};
+            nanosleep(&d, nullptr);
+        }
+        for (int i = 0; i < 3; ++i) {
+            const int64_t v = __atomic_load_n(&e.v[i], __ATOMIC_RELAXED);
+            if (v < acc[i]) acc[i] = v;
+        }
+    }
+    for (int i = 0; i < 3; ++i) out[i] = acc[i];
+    return 0;
+}
+
+int dpow_diag_node_post_at(dpow_node_slot *slot, uint64_t global_idx, int64_t t_ns) {
+    if (!slot) return set_error(DPOW_EINVAL, "dpow_diag_node_post_at: slot is NULL");
+    std::thread([slot, global_idx, t_ns]() {
+        for (;;) {
+            struct timespec ts;
+            clock_gettime(CLOCK_MONOTONIC, &ts);
+            const int64_t left = t_ns - ((int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec);
+            if (left <= 0) break;
+            if (left > 100000) {
+                const struct timespec d = {0, (long)(left - 50000)};
+                nanosleep(&d, nullptr);
+            } else {
+                __builtin_ia32_pause();
+            }
+        }
+        dpow_node_post(slot, global_idx);
+    }).detach();
+    return 0;
 }
 
 void dpow_node_stop(dpow_node_slot *slot) {

@@ -54,7 +54,7 @@ constexpr uint32_t kBop3I = 0x39;  // I = y ^ (x | ~z)
 #define DPOW_SPAN 1
 #endif
 
-// Launches span chunk lengths 1..3 for SH = 0 layouts (plan.cpp lspan_layout; the kernel
+// Launches span chunk lengths 1..3 for SH = 0 layouts (plan.cpp lspan_end; the kernel
 // re-derives the pad and bit-length words per chunk length).  A/B switch: 0 = one launch
 // per chunk length, as in round 2.
 #ifndef DPOW_LSPAN

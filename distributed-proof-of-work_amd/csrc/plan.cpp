@@ -62,7 +62,7 @@ int WindowPlanner::init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, ui
     p_ = (uint32_t)(nonce_len % 64);
     k_ = k_begin;
     k_end_ = k_end;
-    lspan_ok_ = lspan_layout(nonce_len, rbits_, ntz);
+    lspan_end_ = lspan_end(nonce_len, rbits_, ntz);
     // Midstate over nonce-only blocks.
     for (int w = 0; w < 4; ++w) iv_[w] = kMd5IV[w];
     for (size_t b = 0; b < blk_v_; ++b) {
@@ -94,19 +94,23 @@ void WindowPlanner::build_template(uint64_t k, uint32_t L, uint32_t nblk, uint32
     for (uint32_t w = 0; w < 32; ++w) T[w] = w < 16 * nblk ? load_le32(buf + 4 * w) : 0u;
 }
 
-bool lspan_layout(size_t nonce_len, uint32_t rbits, uint32_t ntz) {
+uint64_t lspan_end(size_t nonce_len, uint32_t rbits, uint32_t ntz) {
     // SH = 0: the pads of chunk lengths 0..3 fall in words W0 / W0 + 1, whose K + M the
     // kernel re-derives per segment.  R >= 2: a power-of-two chunk of <= 2R wave-blocks puts
     // the boundaries k = 256 and 65536 (256 R and 65536 R indices) on claim boundaries.
     // A first hit expected within kLspanMaxExpect candidates: the spanning (_ls) kernels
     // hash 1.5-2 % slower than the per-length ones (register assignment), which outweighs
     // the two launches they save (~40 us) once the search is expected to run > ~1.5 ms
-    // ([1,2,3,4]/8: 19.18 -> 19.45 ms merged, profiles/r03_ab_lspan.log).
-    return DPOW_LSPAN && nonce_len % 4 == 0 && rbits >= 1 && expected_first_hit(ntz, rbits) <= kLspanMaxExpect;
+    // ([1,2,3,4]/8: 19.18 -> 19.45 ms merged).  Past that only chunk lengths 1 and 2 share
+    // a launch (k < 2^16, 2^16 R candidates): their two launches cost 17 + 122 us against
+    // 77 us of hashing (profiles/r03_tts_timeline_c.json, [1,2,3,4]/8).
+    // Returns the k below which launches use the chunk-length-0 template (0: none).
+    if (!(DPOW_LSPAN && nonce_len % 4 == 0 && rbits >= 1)) return 0;
+    return expected_first_hit(ntz, rbits) <= kLspanMaxExpect ? 1ull << 24 : 1ull << 16;
 }
 
 bool WindowPlanner::lseg_template(uint64_t k) const {
-    return lspan_ok_ && k < (1ull << 24);
+    return k < lspan_end_;
 }
 
 bool WindowPlanner::next(PlannedLaunch &pl) {
@@ -129,7 +133,7 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     if (!pl.k0 && k >= 1 && lseg_template(k)) {
         // Merge the following chunk lengths (up to 3) with the same block count.
         uint64_t e = ke;
-        while (e < k_end_ && e < (1ull << 24) && nblk_of(chunk_len_of(e)) == nblk) {
+        while (e < k_end_ && e < lspan_end_ && nblk_of(chunk_len_of(e)) == nblk) {
             e = segment_end(e) < k_end_ ? segment_end(e) : k_end_;
             L_last = chunk_len_of(e - 1);
         }
@@ -234,7 +238,7 @@ uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits) {
 }
 
 int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks_out,
-                uint64_t min_chunk) {
+                uint64_t min_chunk, uint64_t claims_per_wave) {
     Launch &L = pl.L;
     constexpr uint64_t wpb = kBlockThreads / 64;
     // Chunk: >= kClaimsPerWave claims per wave of the largest grid the launch gets, over
@@ -249,7 +253,7 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
     if (worker_blocks > max_blocks) worker_blocks = max_blocks;
     uint64_t span_wb = L.n_wblocks;
     if (expect / (uint64_t)kWaveBlock < span_wb) span_wb = expect / (uint64_t)kWaveBlock;
-    uint64_t chunk = span_wb / (worker_blocks * wpb * kClaimsPerWave);
+    uint64_t chunk = span_wb / (worker_blocks * wpb * claims_per_wave);
     if (chunk < min_chunk) chunk = min_chunk;
     if (chunk > kMaxChunk) chunk = kMaxChunk;
     if ((DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) || L.lspan) {
@@ -319,7 +323,7 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits)
     const uint64_t eff = candidates < expect ? candidates : expect;
     if (eff <= kTinyExpect) return kMaxBlocksPerCu < 2 ? kMaxBlocksPerCu : 2;
     if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
-    if (eff <= (1ull << 24)) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
+    if (eff <= kMidExpect) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
 #else
     (void)candidates, (void)ntz, (void)rbits;
 #endif

@@ -26,7 +26,7 @@ uint64_t word2_period(uint32_t sh);
 // The planner may merge chunk lengths 1..3 (k in [1, 2^24)) into one launch: SH = 0
 // layouts, R >= 2, equal block counts (WindowPlanner::next).
 constexpr uint64_t kLspanMaxExpect = 1ull << 28;
-bool lspan_layout(size_t nonce_len, uint32_t rbits, uint32_t ntz);
+uint64_t lspan_end(size_t nonce_len, uint32_t rbits, uint32_t ntz);
 #ifndef DPOW_START_K0
 #define DPOW_START_K0 1  // k = 0 hashed by the search's start kernel (A/B switch)
 #endif
@@ -47,13 +47,13 @@ class WindowPlanner {
 
    private:
     uint32_t nblk_of(uint32_t chunk_len) const;
-    bool lseg_template(uint64_t k) const;  // the launch's template is chunk length 0's (SH = 0, k < 2^24)
+    bool lseg_template(uint64_t k) const;  // the launch's template is chunk length 0's (SH = 0, k < lspan_end_)
     void build_template(uint64_t k, uint32_t chunk_len, uint32_t nblk, uint32_t T[32]) const;
     const uint8_t *nonce_ = nullptr;
     size_t nonce_len_ = 0, blk_v_ = 0;
     uint32_t p_ = 0, ntz_ = 0, rbits_ = 0, base_tb_ = 0;
     uint64_t k_ = 0, k_end_ = 0;
-    bool lspan_ok_ = false;  // launches below k = 2^24 use the chunk-length-0 template and may span
+    uint64_t lspan_end_ = 0;  // launches below this k use the chunk-length-0 template and may span
     uint32_t iv_[4] = {0, 0, 0, 0};
 };
 
@@ -89,9 +89,10 @@ static_assert((kMinChunk & (kMinChunk - 1)) == 0 && (kMaxChunk & (kMaxChunk - 1)
               "chunk bounds are powers of two (segment alignment)");
 // expect: candidates of the launch expected before its first hit (expected_first_hit;
 // ~0 = none): chunks are sized so that >= kClaimsPerWave claims per wave come before it.
-// min_chunk: a power of two (diagnostic override of kMinChunk, dpow_api.cpp).
+// min_chunk: a power of two (diagnostic override of kMinChunk, dpow_api.cpp); claims_per_wave:
+// diagnostic override of kClaimsPerWave.
 int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_t *worker_blocks,
-                uint64_t min_chunk = kMinChunk);
+                uint64_t min_chunk = kMinChunk, uint64_t claims_per_wave = kClaimsPerWave);
 // Mean number of a partition's candidates before its first hit at N trailing zeros.
 uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits);
 
@@ -119,6 +120,12 @@ uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
 // [5,6,7,8]/5 0.040 -> 0.025 ms, fresh N = 5 0.044 -> 0.035 ms, an 8-GPU rank's
 // [1,2,3,4]/6 0.043 -> 0.026 ms.
 constexpr uint64_t kTinyExpect = 1ull << 21;
+// Up to kMidExpect (N = 6 on one GPU, N = 7 on a rank of a 4- or 8-GPU node): 4 workgroups
+// per CU.  The rate is ~6 % below the full grid's, but a rank that another rank's hit
+// stops drains in half the time: stop latency at N = 7 on an 8-GPU rank's window 103 ->
+// 52 us (tools/small_search_probe.py --stop, profiles/r03_stop_probe.json), while the owner's
+// own search is no slower (0.225 -> 0.212 ms).
+constexpr uint64_t kMidExpect = 1ull << 26;
 constexpr uint64_t kTinyChunk = 2;
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits);
 

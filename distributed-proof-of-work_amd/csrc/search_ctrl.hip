@@ -47,7 +47,13 @@ __device__ void md5_block(uint32_t st[4], const uint32_t M[16]) {
 // touches no control block: it runs on the context's second stream beside the search's
 // first md5 launch, and the host consumes its record first (the lowest indices of the
 // window), so a hit here ends the search and the md5 launches are stopped as stale.
+//
+// It runs at the highest wave priority: beside a persistent md5 grid (6 waves per SIMD at
+// priority 1, md5_search_kernel.h) its one workgroup otherwise lost the issue arbitration
+// to the older waves and took 350-430 us for its 256 candidates (profiles/r03_tts_timeline_c.json),
+// which a search -- and an 8-GPU node rank that another rank's hit stops -- waits for.
 __global__ void __launch_bounds__(kBlockThreads) search_k0_kernel(const StartK0 k0) {
+    __builtin_amdgcn_s_setprio(3);
     __shared__ unsigned long long hit;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) hit = kNoHit;

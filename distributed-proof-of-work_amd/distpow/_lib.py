@@ -159,6 +159,9 @@ def lib():
         "dpow_node_slot_reset": (None, [vp]),
         "dpow_node_post": (None, [vp, ctypes.c_uint64]),
         "dpow_node_stop": (None, [vp]),
+        "dpow_node_vote": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                          ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.c_int64]),
         "dpow_secret_from_index": (ctypes.c_int, [ctypes.c_uint64, u8p, szp]),
         "dpow_md5": (None, [ctypes.c_char_p, ctypes.c_size_t, u8p]),
         "dpow_trailing_zero_nibbles": (ctypes.c_uint32, [ctypes.c_char_p]),
@@ -184,6 +187,7 @@ def lib():
                                                 ctypes.c_uint32, ctypes.c_uint32]),
         "dpow_diag_blocks_per_cu": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
         "dpow_diag_search_times": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+        "dpow_diag_node_post_at": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_int64]),
         "dpow_worker_new": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
         "dpow_worker_free": (None, [vp]),
         "dpow_worker_mine": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,

@@ -92,26 +92,57 @@ class NodeBoard:
     and every other rank's running search takes it as its bound while it waits for its
     kernels, so the node stops at its lowest hit without waiting for a batch boundary.
     A cancelled or failed rank raises the slot's stop, which ends every rank's search.
-    The RCCL all-reduce at batch boundaries still decides the answer (the minimum over
-    the ranks, the workerBits = 0 first hit).  The slot of call c + 2 is reset at the
-    end of call c: every rank has passed call c + 1's last all-reduce before any rank
-    uses it, so no reset can race a post.
+    The batch boundary still decides the answer (the minimum over the ranks, the
+    workerBits = 0 first hit): on a shared board it is the node vote (dpow_node_vote, a
+    MIN over the ranks' entries in the same shared memory: microseconds, where an RCCL
+    all-reduce of the 24 bytes plus its host copies costs ~33 us at world 1), else the
+    RCCL all-reduce.  The slot of call c + 2 is reset at the end of call c: every rank
+    has passed call c + 1's last boundary before any rank uses it, so no reset can race
+    a post.
 
     Created collectively (every rank of `group`); None from create() when the ranks do
-    not share one host (then node_mine runs on batch boundaries alone).
+    not share one host (then node_mine runs on RCCL batch boundaries alone).
     """
     SLOTS = 4
     SLOT_BYTES = 64
+    VOTE_BYTES = 64  # dpow_node_vote_entry; two per rank
+    VOTE_TIMEOUT_NS = 120 * 10**9  # a rank that never votes (dead): NodeError after 2 minutes
 
-    def __init__(self, shm=None):
+    def __init__(self, shm=None, world: int = 0, rank: int = 0):
         import ctypes
         self._shm = shm
+        self.world, self.rank = world, rank
         if shm is not None:
             self._base = ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
         else:  # local(): one process's own slots (single-rank use, tools/node_probe.py)
             self._mem = (ctypes.c_uint64 * (self.SLOTS * self.SLOT_BYTES // 8))()
             self._base = ctypes.addressof(self._mem)
+        self._votes = self._base + self.SLOTS * self.SLOT_BYTES
+        self._epoch = 0
         self._calls = 0
+
+    @property
+    def shared(self) -> bool:
+        """The board is mapped by every rank of the node (create()): node_mine votes through it."""
+        return self._shm is not None and self.world > 0
+
+    @classmethod
+    def nbytes(cls, world: int) -> int:
+        return cls.SLOTS * cls.SLOT_BYTES + 2 * world * cls.VOTE_BYTES
+
+    def vote(self, values):
+        """MIN over the node's ranks of three int64 (dpow_node_vote); every rank calls it at
+        the same boundaries, with the same values' meaning, and gets the same result."""
+        import ctypes
+
+        from ._lib import check, lib
+        self._epoch += 1
+        vin = (ctypes.c_int64 * 3)(*values)
+        vout = (ctypes.c_int64 * 3)()
+        rc = lib().dpow_node_vote(self._votes, self.rank, self.world, self._epoch, vin, vout, self.VOTE_TIMEOUT_NS)
+        if rc < 0:
+            raise NodeError(f"rank {self.rank}: node vote failed ({rc}): {lib().dpow_last_error().decode()}")
+        return [int(x) for x in vout]
 
     @classmethod
     def local(cls) -> "NodeBoard":
@@ -143,15 +174,16 @@ class NodeBoard:
         shm = None
         if rank == 0:
             shm = shared_memory.SharedMemory(name=f"dpow_node_{os.getpid()}_{uuid.uuid4().hex[:12]}", create=True,
-                                             size=cls.SLOTS * cls.SLOT_BYTES)
+                                             size=cls.nbytes(world))
             name[0] = shm.name
         dist.broadcast_object_list(name, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         if rank != 0:
             shm = shared_memory.SharedMemory(name=name[0])
-        board = cls(shm)
+        board = cls(shm, world, rank)
         if rank == 0:
             for i in range(cls.SLOTS):
                 lib().dpow_node_slot_reset(board.slot(i))
+            shm.buf[cls.SLOTS * cls.SLOT_BYTES:cls.nbytes(world)] = bytes(2 * world * cls.VOTE_BYTES)
         dist.barrier(group=group)
         if rank == 0:  # every rank has it mapped: nothing is left in /dev/shm, whatever happens next
             shm.unlink()
@@ -216,11 +248,13 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
       hashing; 2^24 k at 8 GPUs).  For T ms of hashing per rank, c T / B + B / 2 is
       smallest near B = sqrt(2 c T), 2.3 ms for N = 9 at 8 GPUs.
 
-    The batch-boundary all-reduce runs whenever a process group is initialised (also at
-    world = 1): MIN over [best index, running, healthy].  A rank whose search raises
-    votes healthy = 0 in the same all-reduce, so no rank is left waiting in a collective
-    the failed rank never joins: the failing rank re-raises its error, the others raise
-    NodeError (coordinator.go:202-206: a missing result is fatal, not silent).
+    The batch boundary is a MIN over [best index, running, healthy] across the ranks: the
+    node vote of a shared board (NodeBoard.vote, every rank on one host), else the
+    all-reduce over the process group whenever one is initialised (also at world = 1).  A
+    rank whose search raises votes healthy = 0 at the same boundary, so no rank is left
+    waiting for a vote the failed rank never casts: the failing rank re-raises its error,
+    the others raise NodeError (coordinator.go:202-206: a missing result is fatal, not
+    silent).
 
     board / attach_fn: the node's shared-memory Found fan-out (NodeBoard); attach_fn(slot)
     attaches a slot address to this rank's search context (Miner.attach_node), None
@@ -237,14 +271,18 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
     if batch_k_max is None:
         batch_k_max = max(1, batch_candidates_max >> (8 - wbits % 9))
     dist_on = dist.is_available() and dist.is_initialized()
-    if device is None:
-        backend = dist.get_backend(group) if dist_on else "gloo"
-        device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    buf = torch.empty(3, dtype=torch.int64, device=device)
-    # With a device buffer (RCCL), a pinned host twin carries the values in and out:
-    # stream-ordered copies around the all-reduce and one stream synchronize per batch.
-    on_gpu = buf.device.type == "cuda"
-    hbuf = torch.empty(3, dtype=torch.int64, pin_memory=True) if on_gpu else buf
+    # The batch boundary: the node vote on a shared board (all ranks on one host), else the
+    # all-reduce over the process group (RCCL with the "nccl" backend).
+    board_vote = board is not None and board.shared and board.world == world
+    if not board_vote:
+        if device is None:
+            backend = dist.get_backend(group) if dist_on else "gloo"
+            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        buf = torch.empty(3, dtype=torch.int64, device=device)
+        # With a device buffer (RCCL), a pinned host twin carries the values in and out:
+        # stream-ordered copies around the all-reduce and one stream synchronize per batch.
+        on_gpu = buf.device.type == "cuda"
+        hbuf = torch.empty(3, dtype=torch.int64, pin_memory=True) if on_gpu else buf
     slot = board.begin() if board is not None else None
     if slot is not None:
         attach_fn(slot)
@@ -272,16 +310,19 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
             # node search): voting it too ends the batch for a rank that was bounded by it even
             # without a process group, and the all-reduce's minimum is unchanged.
             vote = min(mine, board.best(slot)) if slot is not None else mine
-            hbuf[0], hbuf[1], hbuf[2] = vote, running, 0 if err is not None else 1
-            if on_gpu:
-                buf.copy_(hbuf, non_blocking=True)
-            if dist_on:
-                dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
-            if on_gpu:
-                hbuf.copy_(buf, non_blocking=True)
-                torch.cuda.current_stream(buf.device).synchronize()
+            if board_vote:
+                best, all_running, healthy = board.vote([vote, running, 0 if err is not None else 1])
+            else:
+                hbuf[0], hbuf[1], hbuf[2] = vote, running, 0 if err is not None else 1
+                if on_gpu:
+                    buf.copy_(hbuf, non_blocking=True)
+                if dist_on:
+                    dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
+                if on_gpu:
+                    hbuf.copy_(buf, non_blocking=True)
+                    torch.cuda.current_stream(buf.device).synchronize()
+                best, all_running, healthy = (int(x) for x in hbuf.tolist())
             batches += 1
-            best, all_running, healthy = (int(x) for x in hbuf.tolist())
             if not healthy:
                 if err is not None:
                     raise err

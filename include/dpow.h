@@ -140,6 +140,24 @@ void dpow_node_post(dpow_node_slot *slot, uint64_t global_idx);
 /* Raise the slot's stop. */
 void dpow_node_stop(dpow_node_slot *slot);
 
+/* Node vote (round 3): node_mine's batch boundary among the G ranks of one host, through
+ * the same shared memory instead of a collective -- MIN over the ranks of three int64
+ * values ([best index, running, healthy]); every rank gets the same result.  `votes` is
+ * an array of world * 2 dpow_node_vote_entry (zeroed before the first vote), shared by the
+ * ranks; each rank votes once per boundary with the same increasing epoch (1, 2, ...),
+ * into entry [rank][epoch % 2] (a rank is at most one boundary ahead of the slowest),
+ * then waits for every rank's entry of that epoch.  An RCCL all-reduce of the same 24
+ * bytes costs 33 us at world 1 on an MI355X (tests/test_gpu_rccl.py); this costs the
+ * slowest rank's arrival plus a cache-line transfer.  Returns 0, or DPOW_EPROTO (dpow_worker.h) when some
+ * rank's vote has not arrived within timeout_ns (a dead rank; the node's search is lost). */
+typedef struct dpow_node_vote_entry {
+    uint64_t epoch;
+    int64_t v[3];
+    uint64_t pad[4];   /* one 64-byte line per entry */
+} dpow_node_vote_entry;
+int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, uint64_t epoch,
+                   const int64_t in[3], int64_t out[3], int64_t timeout_ns);
+
 /* ---------------------------------------------------------------------------
  * Host helpers (no GPU needed).
  * ------------------------------------------------------------------------- */

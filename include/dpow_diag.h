@@ -83,8 +83,15 @@ uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t wor
  * first md5 launch's record slot retired, [7] unused.
  * Environment overrides read at dpow_open (A/B runs only): DPOW_DIAG_POLL_WB (wave-blocks
  * per poll group), DPOW_DIAG_BPC (worker workgroups per CU), DPOW_DIAG_MIN_CHUNK (minimum
- * wave-blocks per claim, a power of two).  Returns 0, or < 0 on error. */
+ * wave-blocks per claim, a power of two), DPOW_DIAG_CPW (big claims per wave: the chunk
+ * sizing).  Returns 0, or < 0 on error. */
 int dpow_diag_search_times(struct dpow_ctx *ctx, int64_t out[8]);
+
+/* Node emulation on one GPU (tools/node_probe.py): post global_idx to a node slot
+ * (dpow_node_post) from a detached native thread at CLOCK_MONOTONIC time t_ns, as another
+ * rank's process would -- off the caller's thread and its Python interpreter lock.
+ * Returns 0, or < 0 on error. */
+int dpow_diag_node_post_at(struct dpow_node_slot *slot, uint64_t global_idx, int64_t t_ns);
 
 #ifdef __cplusplus
 }

@@ -58,12 +58,13 @@ def test_plan_window_segments():
     for p in pl:
         assert (p.nblk, p.w0, p.sh) == (1, 1, 0)  # 4-byte nonce: V lands in word 1
         assert p.i_begin == p.k_begin * 256 and p.i_end == p.k_end * 256
-    # a first hit expected late (N = 8 at R = 256: 2^32 candidates) keeps one launch per
-    # chunk length: the per-length kernels hash ~2 % faster (plan.cpp lspan_layout)
+    # a first hit expected late (N = 8 at R = 256: 2^32 candidates) merges chunk lengths 1 and
+    # 2 only: the chunk length 3 launch runs the per-length kernel, which hashes ~2 % faster
+    # (plan.cpp lspan_end)
     assert [(p.k_begin, p.k_end) for p in distpow.plan_window(b"\x01\x02\x03\x04", 0, 0, 0, 70000, 8)] == \
-        [(0, 1), (1, 256), (256, 65536), (65536, 70000)]
+        [(0, 1), (1, 65536), (65536, 70000)]
     assert len(distpow.plan_window(b"\x01\x02\x03\x04", 0, 0, 0, 70000, 7)) == 2
-    assert len(distpow.plan_window(b"\x01\x02\x03\x04", 5, 3, 0, 70000, 8)) == 4  # 2^29 > 2^28
+    assert len(distpow.plan_window(b"\x01\x02\x03\x04", 5, 3, 0, 70000, 8)) == 3  # 2^29 > 2^28
     # a window inside the merged range, and one from k = 300
     assert [(p.k_begin, p.k_end) for p in distpow.plan_window(b"\x01\x02\x03\x04", 0, 0, 200, 70000)] == \
         [(200, 70000)]

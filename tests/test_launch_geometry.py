@@ -148,11 +148,11 @@ def test_grid_policy_for_short_launches():
     from distpow._lib import lib
     f = lib().dpow_diag_blocks_per_cu
     assert f(1 << 36, 32, 0) == 6 and f(1 << 36, 32, 3) == 6       # the bench sweep, 1 and 8 GPUs
-    assert f(1 << 22, 32, 0) == 3 and f(1 << 24, 32, 0) == 4 and f((1 << 24) + 1, 32, 0) == 6
+    assert f(1 << 22, 32, 0) == 3 and f(1 << 26, 32, 0) == 4 and f((1 << 26) + 1, 32, 0) == 6
     assert f(1 << 21, 32, 0) == 2 and f((1 << 21) + 1, 32, 0) == 3  # tiny launches (plan.h kTinyExpect)
     assert f(1 << 32, 6, 0) == 4 and f(1 << 32, 5, 0) == 2 and f(1 << 32, 7, 0) == 6  # 16^N expected
     assert f(1 << 32, 6, 3) == 2        # 16^6 * 32 / 256 = 2^21 candidates of a workerBits-3 partition
-    assert f(1 << 32, 7, 3) == 6        # 2^25
+    assert f(1 << 32, 7, 3) == 4 and f(1 << 32, 7, 2) == 4 and f(1 << 32, 7, 1) == 6  # 2^25 / 2^26 / 2^27
     assert f(1 << 32, 0, 0) == 2 and f(0, 32, 0) == 2
     for n in range(0, 40, 3):  # never more than the full grid, monotone in the launch size
         seq = [f(1 << n, z, 0) for z in range(0, 34)]

@@ -339,3 +339,66 @@ def test_node_mine_world1_group_runs_the_collective():
         dist.destroy_process_group()
     assert r.status == 1 and r.global_idx == 97 and r.owner == 0
     assert calls == [[97, 1, 1]]
+
+
+def _worker_vote(rank, world, shm_name, rounds, out_q):
+    """dpow_node_vote from one process: every epoch votes [rank-dependent, ...] values and
+    must get the MIN over all ranks; rank 0 is slow on odd epochs (the others wait)."""
+    import ctypes
+    import sys
+    import time
+    from multiprocessing import shared_memory
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+    from distpow._lib import lib
+    shm = shared_memory.SharedMemory(name=shm_name)
+    base = ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+    got = []
+    for e in range(1, rounds + 1):
+        if rank == 0 and e % 2:
+            time.sleep(0.002)
+        vin = (ctypes.c_int64 * 3)(1000 * e + rank, e % world == rank, -rank)
+        vout = (ctypes.c_int64 * 3)()
+        rc = lib().dpow_node_vote(base, rank, world, e, vin, vout, 10 * 10**9)
+        got.append((rc, list(vout)))
+    out_q.put((rank, got))
+    del base
+    shm.close()
+
+
+def test_node_vote_shared_memory():
+    """The node vote (include/dpow.h dpow_node_vote): MIN over every rank's values at each
+    epoch, the same on every rank, with ranks at most one epoch apart (double-buffered
+    entries); and a rank whose peer never votes gets DPOW_EPROTO at its timeout."""
+    import ctypes
+    from multiprocessing import shared_memory
+    world, rounds = 4, 200
+    shm = shared_memory.SharedMemory(create=True, size=2 * world * 64)
+    try:
+        shm.buf[:2 * world * 64] = bytes(2 * world * 64)
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_worker_vote, args=(r, world, shm.name, rounds, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        outs = dict(q.get(timeout=120) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        for r in range(world):
+            for e, (rc, v) in enumerate(outs[r], start=1):
+                assert rc == 0 and v == [1000 * e, 0 if world > 1 else 1, -(world - 1)], (r, e, v)
+        # a peer that never votes: DPOW_EPROTO (-6) after the timeout, not a hang
+        here = os.path.dirname(os.path.abspath(__file__))
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+        from distpow._lib import lib
+        shm.buf[:2 * world * 64] = bytes(2 * world * 64)
+        base = ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+        vin, vout = (ctypes.c_int64 * 3)(1, 1, 1), (ctypes.c_int64 * 3)()
+        assert lib().dpow_node_vote(base, 0, 2, 1, vin, vout, 50 * 10**6) == -6
+        assert b"did not vote" in lib().dpow_last_error()
+        del base
+    finally:
+        shm.close()
+        shm.unlink()

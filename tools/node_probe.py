@@ -11,9 +11,10 @@ stops.  The node's time is therefore the slowest rank's: the owner's time to its
 hit, or a non-owner's time to notice the posted hit and drain.  This runs
 
   1. the owner alone (world = G, no process group): t_owner;
-  2. every other rank alone, with a thread that posts the owner's hit to the board
-     slot when the owner's search posted it (its dpow_search returning FOUND, measured
-     in step 1), counted from the rank's own start, as the owner's process would;
+  2. every other rank alone, with a native thread (dpow_diag_node_post_at) that posts the
+     owner's hit to the board slot when the owner's search posted it (its dpow_search
+     returning FOUND, measured in step 1), counted from the rank's own start, as the
+     owner's process would;
 
 and reports max over ranks, next to one GPU's Miner.mine (G1) and the world-1 RCCL
 batch boundary (pinned copy + all-reduce + copy + synchronize), which the real node
@@ -24,7 +25,6 @@ with the whole GPU, so this is the node's time without its RCCL collective; the
 import json
 import os
 import sys
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -47,7 +47,6 @@ def main():
             ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5)]
     exp = {(tuple(e["nonce"]), e["ntz"]): e["global_idx"] for e in gold["first_hits"] + gold["deep_hits"]}
     want += [(list(n), 9) for (n, z) in exp if z == 9 and n not in ((1, 2, 3, 4), (5, 6, 7, 8), (2, 2, 2, 2))]
-    sys.setswitchinterval(1e-5)
     dev = torch.device("cuda", 0)
     out = {"note": __doc__.strip().splitlines()[0], "g1_ms": {}, "node_ms": {}}
     board = NodeBoard.local()
@@ -70,35 +69,22 @@ def main():
         def search_timed(*a):
             r = search(*a)
             if r.status == distpow.FOUND:
-                found_at["t"] = time.perf_counter()  # dpow_search posted its hit just before returning
+                found_at["t"] = time.perf_counter_ns() / 1e9  # dpow_search posted its hit just before returning
             return r
 
         def run_rank(nonce, n, rank, G, post_after_s=None, g=None):
             slot = board.begin()
-            stop = threading.Event()
-
-            def poster(t0):
-                # sleep, then spin the last 0.3 ms (a short GIL switch interval keeps the
-                # spinning thread from delaying the rank's own Python between its searches)
-                left = post_after_s - (time.perf_counter() - t0)
-                if left > 3e-4:
-                    stop.wait(left - 3e-4)
-                while time.perf_counter() - t0 < post_after_s and not stop.is_set():
-                    pass
-                lib.dpow_node_post(slot, g)
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            th = None
-            if post_after_s is not None:
-                th = threading.Thread(target=poster, args=(t0,))
-                th.start()
             found_at.clear()
+            t0 = time.perf_counter_ns()  # CLOCK_MONOTONIC
+            if post_after_s is not None:
+                # the owner's process posts its hit at t0 + post_after_s: a native thread, off
+                # this interpreter (a Python poster thread took the GIL and its start alone
+                # cost the rank 50-100 us)
+                lib.dpow_diag_node_post_at(slot, g, t0 + int(post_after_s * 1e9))
             res = node_mine(search_timed, nonce, n, rank, G, device=dev, board=board, attach_fn=m.attach_node)
-            dt = time.perf_counter() - t0
-            t_post = found_at.get("t", t0 + dt) - t0
-            stop.set()
-            if th:
-                th.join()
+            dt = (time.perf_counter_ns() - t0) / 1e9
+            t_post = found_at.get("t", t0 / 1e9 + dt) - t0 / 1e9
             return res, dt, t_post
 
         for G in (2, 4, 8):

@@ -201,8 +201,8 @@ def lib():
         "dpow_worker_active_tasks": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
-        if LIB_OVERRIDE and name.startswith("dpow_diag_") and not hasattr(L, name):
-            continue  # an older A/B build (tools/ab_variants.py) may lack a newer diagnostic
+        if LIB_OVERRIDE and not hasattr(L, name):
+            continue  # an older A/B build (tools/ab_variants.py) may lack a newer entry point
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

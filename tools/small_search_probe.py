@@ -50,7 +50,8 @@ def stop_cases(m, lib, runs=7):
     slot_mem = (ctypes.c_uint64 * 8)()
     slot = ctypes.addressof(slot_mem)
     out = {}
-    for label, n, k0 in (("stop N=7", 7, 1 << 24), ("stop N=8", 8, 1 << 24), ("stop N=32", 32, 1 << 24)):
+    for label, n, k0 in (("stop N=6", 6, 1 << 24), ("stop N=7", 7, 1 << 24), ("stop N=8", 8, 1 << 24),
+                         ("stop N=32", 32, 1 << 24)):
         ms, tls = [], []
         for _ in range(runs):
             lib.dpow_node_slot_reset(slot)

@@ -163,7 +163,9 @@ struct SearchWait {
 struct dpow_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    Ctrl *d_ctrl = nullptr;  // kCtrlRing control blocks (kCtrlStride apart); ctrl_idx's is clean
+    Ctrl *d_ctrl = nullptr;  // kCtrlRing control blocks (kCtrlStride apart, aligned to the ring's size);
+                             //  ctrl_idx's is clean
+    Ctrl *d_ctrl_alloc = nullptr;
     uint32_t ctrl_idx = 0;
     unsigned long long *d_claims = nullptr;  // kClaimRing slots of kClaimSlot claim counters
     Snap *h_snap = nullptr;        // kRing completion records: pinned, host-coherent, mapped
@@ -582,7 +584,7 @@ int dpow_open(int device, dpow_ctx **out) {
     }
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipMalloc(&c->d_ctrl, kCtrlRing * kCtrlStride * sizeof(Ctrl))) != hipSuccess ||
+        (e = hipMalloc(&c->d_ctrl_alloc, 2 * kCtrlRing * kCtrlStride * sizeof(Ctrl))) != hipSuccess ||
         (e = hipMalloc(&c->d_claims, kClaimRing * kClaimSlot * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_snap, kRing * sizeof(Snap), hipHostMallocCoherent | hipHostMallocMapped)) !=
             hipSuccess ||
@@ -591,6 +593,10 @@ int dpow_open(int device, dpow_ctx **out) {
         (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_cancel), c->h_cancel, 0)) != hipSuccess) {
         dpow_close(c);
         return hip_fail(e, "dpow_open: allocation");
+    }
+    {   // the control-block ring, aligned to its size (publish() derives the next block's address)
+        const uintptr_t rb = kCtrlRing * kCtrlStride * sizeof(Ctrl);
+        c->d_ctrl = reinterpret_cast<Ctrl *>((reinterpret_cast<uintptr_t>(c->d_ctrl_alloc) + rb - 1) & ~(rb - 1));
     }
     memset(c->h_snap, 0, kRing * sizeof(Snap));
     memset(c->h_cancel, 0, kCancelPage);
@@ -612,7 +618,7 @@ void dpow_close(dpow_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->d_ctrl) (void)hipFree(c->d_ctrl);
+    if (c->d_ctrl_alloc) (void)hipFree(c->d_ctrl_alloc);
     if (c->d_claims) (void)hipFree(c->d_claims);
     if (c->h_snap) (void)hipHostFree(c->h_snap);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);

@@ -88,6 +88,7 @@ struct Ctrl {
 };
 constexpr uint32_t kCtrlRing = 4;
 constexpr uint32_t kCtrlStride = 128 / sizeof(Ctrl);  // Ctrl units between ring entries
+static_assert((kCtrlRing & (kCtrlRing - 1)) == 0 && 128 % sizeof(Ctrl) == 0, "the ring is aligned to its size");
 
 // Host-visible completion record of one launch (pinned, host-coherent, mapped).
 // The launch's last retiring workgroup writes it: the
@@ -134,7 +135,8 @@ struct Launch {
     unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;              // this search's control block (clean at its first launch)
-    Ctrl *ctrl_next;         // the next search's: reset by this launch's last workgroup
+    Ctrl *ctrl_next;         // the next search's: reset by this launch's last workgroup (which derives it
+                             //  from ctrl: the ring is aligned to its size; kept here for the host's checks)
     const uint32_t *cancel;  // device-visible alias of the pinned host cancel flag
     const uint32_t *stale;   // pinned: launches with seq <= *stale (mod 2^32) belong to a cancelled search
     const unsigned long long *ext_bound;  // pinned: the bound dpow_search_bound injected (the watcher relays it)

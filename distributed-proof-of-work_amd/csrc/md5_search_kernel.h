@@ -995,7 +995,9 @@ DPOW_DEV void search_body(const Launch &L) {
         // Down-counters keep the loop's live SGPRs at a plain loop's count.
         uint64_t i0 = i_first;
         uint32_t left = nb;
-        const uint32_t poll_wb = L.poll_wb;
+        // (two final blocks: the compile-time group -- a runtime one kept one more SGPR live
+        // across the hash loop, where their K + M constants already fill the budget)
+        const uint32_t poll_wb = NBLK == 2 ? (uint32_t)DPOW_POLL_WB : L.poll_wb;
         for (;;) {
             uint32_t q = left < poll_wb ? left : poll_wb;
 #if DPOW_SPAN

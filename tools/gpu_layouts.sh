@@ -1,5 +1,5 @@
 # GPU tests, the layout check against the oracle (tests/soak/layout_check.py) and a layout
-# sweep (tools/layout_sweep.py), also of an A/B build abx/libdpow_r02.so if present, through gpurun:
+# sweep (tools/layout_sweep.py) through gpurun:
 #   gpurun --timeout 900 -- bash tools/gpu_layouts.sh <tag> [log2 rounds lengths]
 set -o pipefail
 tag=${1:-layouts}; shift
@@ -9,8 +9,3 @@ timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeou
 tail -1 $out/pytest.log
 timeout -k 10 300 python3 -u tests/soak/layout_check.py > $out/layout_check.json 2> $out/layout_check.err &&
 timeout -k 10 600 python3 -u tools/layout_sweep.py "$@" > $out/layout_sweep.log 2> $out/layout_sweep.err
-for lib in abx/libdpow_r02.so; do
-    [ -f "$lib" ] || continue
-    b=$(basename $lib .so)
-    DPOW_LIB_PATH=$lib timeout -k 10 600 python3 -u tools/layout_sweep.py "$@" > $out/layout_sweep_$b.log 2> $out/layout_sweep_$b.err || exit $?
-done

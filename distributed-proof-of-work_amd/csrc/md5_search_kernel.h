@@ -670,14 +670,19 @@ DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_
 // It also resets the next search's control block (ctrl_next): every launch of this search
 // runs before any of the next one's (stream order), so the next search needs no reset
 // kernel in front of its first launch.
-// (ctrl_next is derived from ctrl -- the ring is kCtrlRing * 128 bytes, aligned to its size
-// -- rather than passed: one more pointer live across the hash loop put 1-5 SGPR spill
-// reloads into every wave-block of the two-block kernels, tools/isa_loop.py.)
-__device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim) {
-    constexpr uintptr_t kRingBytes = kCtrlRing * kCtrlStride * sizeof(Ctrl);
-    const uintptr_t a = reinterpret_cast<uintptr_t>(ctrl);
-    Ctrl *const ctrl_next =
-        reinterpret_cast<Ctrl *>((a & ~(kRingBytes - 1)) | ((a + kCtrlStride * sizeof(Ctrl)) & (kRingBytes - 1)));
+// (The two-block kernels pass ctrl_next = null and publish() derives it from ctrl -- the
+// ring is kCtrlRing * 128 bytes, aligned to its size: one more pointer live across their
+// hash loop, which sits at the SGPR limit, put SGPR spill reloads into it.  The one-block
+// kernels pass it: deriving it there moved the sweep kernel's register assignment and cost
+// it 0.6 % (218.1 -> 216.8 GH/s, profiles/r03_ab_publish.log).)
+__device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim,
+                                                  Ctrl *ctrl_next) {
+    if (ctrl_next == nullptr) {
+        constexpr uintptr_t kRingBytes = kCtrlRing * kCtrlStride * sizeof(Ctrl);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(ctrl);
+        ctrl_next =
+            reinterpret_cast<Ctrl *>((a & ~(kRingBytes - 1)) | ((a + kCtrlStride * sizeof(Ctrl)) & (kRingBytes - 1)));
+    }
     // Every workgroup has left its claim loop: recycle the counter slot (claim[1]: the
     // launch's start time, written by the watcher).
     const unsigned long long t_start = __hip_atomic_load(&claim[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1092,7 +1097,7 @@ DPOW_DEV void search_body(const Launch &L) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim);
+        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, NBLK == 2 ? nullptr : L.ctrl_next);
     }
 }
 

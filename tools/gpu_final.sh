@@ -1,0 +1,7 @@
+# Final-build evidence through gpurun: GPU tests, the driver's default bench line, the
+# time-to-secret timeline, the per-wave trace, the emulated node (tools/gpu_evidence.sh),
+# then the rocprofv3 kernel-trace + PMC passes of the bench (tools/profile_gpu.sh).
+#   gpurun --timeout 1200 -- bash tools/gpu_final.sh <tag>
+set -o pipefail
+tag=${1:-final}
+bash tools/gpu_evidence.sh $tag && bash tools/profile_gpu.sh $tag pmc > gpurun_out/$tag/profile.list 2>&1

@@ -274,7 +274,10 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
     # The batch boundary: the node vote on a shared board (all ranks on one host), else the
     # all-reduce over the process group (RCCL with the "nccl" backend).
     board_vote = board is not None and board.shared and board.world == world
-    if not board_vote:
+    # no process group and no shared board (one rank alone, tools/node_probe.py): the
+    # boundary is this rank's own values
+    local_only = not board_vote and not dist_on
+    if not board_vote and not local_only:
         if device is None:
             backend = dist.get_backend(group) if dist_on else "gloo"
             device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
@@ -312,6 +315,8 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
             vote = min(mine, board.best(slot)) if slot is not None else mine
             if board_vote:
                 best, all_running, healthy = board.vote([vote, running, 0 if err is not None else 1])
+            elif local_only:
+                best, all_running, healthy = vote, running, 0 if err is not None else 1
             else:
                 hbuf[0], hbuf[1], hbuf[2] = vote, running, 0 if err is not None else 1
                 if on_gpu:

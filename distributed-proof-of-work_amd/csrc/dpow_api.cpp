@@ -183,7 +183,6 @@ struct dpow_ctx {
     std::mutex bound_mu;
     bool searching = false;                      // under bound_mu
     std::atomic<uint64_t> ext_bound{DPOW_NO_HIT};  // the lowest bound injected into the running search
-    hipStream_t aux_stream = nullptr;  // the k = 0 kernel, beside the search's first md5 launch
     // Node slot (dpow_node_attach): shared by the ranks of one node, polled while a
     // search waits for its records.
     dpow_node_slot *node = nullptr;
@@ -325,27 +324,17 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     PlannedLaunch pl;
     bool have = planner.next(pl);
     c->diag_t[4] = now_ns() - sw.t0;
-    // A window holding k = 0 starts with the k = 0 kernel (search_ctrl.hip) on the second
-    // stream, beside the first md5 launch: launch 0 of the search, with a completion record
-    // of its own that holds its own first hit only.  It is queued right after the first md5
-    // launch (or alone, when the window holds no other k): that launch is the longer one.
+    // A window holding k = 0 starts with the k = 0 kernel (search_ctrl.hip), ahead of the
+    // first md5 launch on the search stream: launch 0 of the search, with a completion record
+    // of its own that holds its own first hit only.  (On a second stream beside the first md5
+    // launch it started 2-4 us sooner, but one more busy device queue per process pushed 8
+    // processes sharing a GPU into queue oversubscription: profiles/r03_rehearsal_queues.json.)
     hipError_t e = hipSuccess;
-    StartK0 k0{};
-    bool k0_pending = false;
-    auto queue_k0 = [&]() -> int {
-        if (!k0_pending) return 0;
-        k0_pending = false;
-        LaunchSlot &k0slot = c->slots[seq0 % kRing];
-        e = search_k0(k0, c->aux_stream);
-        if (e != hipSuccess) return hip_fail(e, "search_k0");
-        k0slot.in_flight = true;
-        c->diag_t[0] = now_ns() - sw.t0;
-        return 0;
-    };
     if (have && pl.k0) {
         LaunchSlot &k0slot = c->slots[seq0 % kRing];
         if ((rc = retire_slot(c, k0slot)) < 0) return rc;
         c->diag_t[5] = now_ns() - sw.t0;
+        StartK0 k0{};
         k0.r = (uint32_t)(pl.L.i_end - pl.L.i_begin);
         k0.base_tb = pl.L.base_tb;
         k0.nblk = pl.info.nblk;
@@ -355,11 +344,14 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         k0.snap = c->d_snap + seq0 % kRing;
         memcpy(k0.iv, pl.L.iv, sizeof k0.iv);
         memcpy(k0.T, pl.L.T, sizeof k0.T);
-        k0_pending = true;
+        e = search_k0(k0, c->stream);
+        if (e != hipSuccess) return hip_fail(e, "search_k0");
+        c->diag_t[0] = now_ns() - sw.t0;
+        k0slot.in_flight = true;
         k0slot.seq = seq0;
         k0slot.candidates = k0.r;
         k0slot.g_end = 1ull << 8;
-        k0slot.stream = c->aux_stream;
+        k0slot.stream = c->stream;
         c->seq = seq0 + 1;
         launched = 1;
         have = planner.next(pl);
@@ -509,7 +501,6 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         if (e != hipSuccess) return hip_fail(e, "search_launch");
         if (!md5_queued) c->diag_t[1] = now_ns() - sw.t0;
         md5_queued = true;
-        if (k0_pending && (rc = queue_k0()) < 0) return rc;
         slot.seq = seq;
         slot.in_flight = true;
         slot.candidates = L.i_end - L.i_begin;
@@ -522,7 +513,6 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
                      (int64_t)((double)slot.candidates * (double)share / kEstRate * 1e9);
         have = planner.next(pl);
     }
-    if (k0_pending && (rc = queue_k0()) < 0) return rc;  // no md5 launch was queued
     while (status == DPOW_EXHAUSTED && consumed < launched) {  // the window is queued: drain in order
         const int r = consume(consumed);
         if (r < 0) return r;
@@ -583,7 +573,6 @@ int dpow_open(int device, dpow_ctx **out) {
         if (v && !(v & (v - 1))) c->min_chunk_override = v;
     }
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&c->d_ctrl_alloc, 2 * kCtrlRing * kCtrlStride * sizeof(Ctrl))) != hipSuccess ||
         (e = hipMalloc(&c->d_claims, kClaimRing * kClaimSlot * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_snap, kRing * sizeof(Snap), hipHostMallocCoherent | hipHostMallocMapped)) !=
@@ -601,14 +590,16 @@ int dpow_open(int device, dpow_ctx **out) {
     memset(c->h_snap, 0, kRing * sizeof(Snap));
     memset(c->h_cancel, 0, kCancelPage);
     *bound_word(c) = DPOW_NO_HIT;
-    {   // clean control blocks and zero claim counters (the launches keep them so)
-        std::vector<Ctrl> ring(kCtrlRing * kCtrlStride, Ctrl{kNoHit, 0u, 0u});
-        if ((e = hipMemcpy(c->d_ctrl, ring.data(), ring.size() * sizeof(Ctrl), hipMemcpyHostToDevice)) != hipSuccess ||
-            (e = hipMemset(c->d_claims, 0, kClaimRing * kClaimSlot * sizeof(unsigned long long))) != hipSuccess ||
-            (e = hipDeviceSynchronize()) != hipSuccess) {
-            dpow_close(c);
-            return hip_fail(e, "dpow_open: control state");
-        }
+    // Clean control blocks and zero claim counters (the launches keep them so): a kernel on
+    // the context's own stream, which stays the only device queue a context uses (no null-
+    // stream copy: with 8 processes sharing one GPU, every extra queue a process keeps busy
+    // pushed the device into queue oversubscription, whose time slices held each search
+    // ~10 ms, profiles/r03_rehearsal_queues.json).
+    if ((e = context_init(c->d_ctrl, kCtrlRing * kCtrlStride, c->d_claims, (uint32_t)(kClaimRing * kClaimSlot),
+                          c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        dpow_close(c);
+        return hip_fail(e, "dpow_open: control state");
     }
     *out = c;
     return 0;
@@ -623,10 +614,6 @@ void dpow_close(dpow_ctx *c) {
     if (c->h_snap) (void)hipHostFree(c->h_snap);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->aux_stream) {
-        (void)hipStreamSynchronize(c->aux_stream);
-        (void)hipStreamDestroy(c->aux_stream);
-    }
     for (void *p : c->registered) (void)hipHostUnregister(p);
     delete c;
 }

@@ -50,5 +50,9 @@ struct StartK0 {
     uint32_t T[32];    // their words, threadByte zeroed (plan.cpp build_template)
 };
 hipError_t search_k0(const StartK0 &k0, hipStream_t stream);
+// A context's initial control state (search_ctrl.hip): n_ctrl clean control blocks, n_claims
+// zero claim counters.
+hipError_t context_init(Ctrl *ctrl, uint32_t n_ctrl, unsigned long long *claims, uint32_t n_claims,
+                        hipStream_t stream);
 
 }  // namespace dpow

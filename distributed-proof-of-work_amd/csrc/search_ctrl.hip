@@ -3,9 +3,9 @@
 // k = 0 is the one chunk whose message layout (msg = nonce || threadByte, the 0x80 pad
 // right behind it) differs from every other chunk's within a wave: a wave of an md5
 // launch holds 64 / R consecutive k, so for R <= 64 it would mix k = 0 and k = 1.  Its
-// R <= 256 candidates are hashed here instead, one per thread, on the context's second
-// stream beside the search's first md5 launch (which starts at k = 1 and may span chunk
-// lengths 1..3: plan.cpp).  (Round 3 start: this kernel also reset the control block and
+// R <= 256 candidates are hashed here instead, one per thread, on the search stream ahead
+// of the search's first md5 launch (which starts at k = 1 and may span chunk lengths 1..3:
+// plan.cpp).  (Round 3 start: this kernel also reset the control block and
 // claim counters, in front of the first md5 launch on the same stream -- 15 us on every
 // search's time-to-secret path; the launches now reset the next search's control block
 // themselves, md5_search_kernel.h publish().)
@@ -44,16 +44,10 @@ __device__ void md5_block(uint32_t st[4], const uint32_t M[16]) {
 
 // The k = 0 candidates, one per thread (worker.go:318-356 for chunk_0 = []: msg = nonce ||
 // threadByte), and the kernel's own completion record: {its first hit, or kNoHit}.  It
-// touches no control block: it runs on the context's second stream beside the search's
-// first md5 launch, and the host consumes its record first (the lowest indices of the
-// window), so a hit here ends the search and the md5 launches are stopped as stale.
-//
-// It runs at the highest wave priority: beside a persistent md5 grid (6 waves per SIMD at
-// priority 1, md5_search_kernel.h) its one workgroup otherwise lost the issue arbitration
-// to the older waves and took 350-430 us for its 256 candidates (profiles/r03_tts_timeline_c.json),
-// which a search -- and an 8-GPU node rank that another rank's hit stops -- waits for.
+// touches no control block; the host consumes its record first (the lowest indices of the
+// window), so a hit here ends the search and the md5 launches queued behind it are
+// stopped as stale.
 __global__ void __launch_bounds__(kBlockThreads) search_k0_kernel(const StartK0 k0) {
-    __builtin_amdgcn_s_setprio(3);
     __shared__ unsigned long long hit;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) hit = kNoHit;
@@ -86,7 +80,21 @@ __global__ void __launch_bounds__(kBlockThreads) search_k0_kernel(const StartK0 
         __hip_atomic_store(&k0.snap->seq, k0.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
+__global__ void context_init_kernel(Ctrl *ctrl, uint32_t n_ctrl, unsigned long long *claims, uint32_t n_claims) {
+    for (uint32_t i = threadIdx.x; i < n_ctrl; i += blockDim.x) {
+        ctrl[i].best = kNoHit;
+        ctrl[i].stop = 0u;
+        ctrl[i].done = 0u;
+    }
+    for (uint32_t i = threadIdx.x; i < n_claims; i += blockDim.x) claims[i] = 0ull;
+}
 }  // namespace
+
+hipError_t context_init(Ctrl *ctrl, uint32_t n_ctrl, unsigned long long *claims, uint32_t n_claims,
+                        hipStream_t stream) {
+    hipLaunchKernelGGL(context_init_kernel, dim3(1), dim3(kBlockThreads), 0, stream, ctrl, n_ctrl, claims, n_claims);
+    return hipGetLastError();
+}
 
 hipError_t search_k0(const StartK0 &k0, hipStream_t stream) {
     hipLaunchKernelGGL(search_k0_kernel, dim3(1), dim3(kBlockThreads), 0, stream, k0);

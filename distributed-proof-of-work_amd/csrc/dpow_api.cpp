@@ -824,6 +824,7 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
             d.chunk_tail = pl.L.chunk_tail;
             d.rbits = pl.L.rbits;
             d.wave_block = kWaveBlock;
+            d.n_static = pl.L.n_static;
         }
         ++n;
     }

@@ -65,6 +65,7 @@ typedef struct dpow_diag_launch {
     uint32_t chunk, chunk_tail;   /* wave-blocks per big / tail claim */
     uint32_t rbits;               /* R = 2^rbits thread bytes per k */
     uint32_t wave_block;          /* local indices per wave-block */
+    uint64_t n_static;            /* claims handed out by wave index (the "_ls" kernels' static first claims) */
 } dpow_diag_launch;
 int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte,
                               uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,

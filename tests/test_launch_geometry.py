@@ -7,7 +7,8 @@ dpow_diag_launch_geometry.  Invariants the kernel relies on (md5_search_kernel.h
 * every claim counter that holds a claim has a worker workgroup (block b serves
   counter (b - 1) % 8), and the grid never exceeds max_blocks;
 * in a launch that spans 2^24-k segments no claim straddles a segment boundary (the
-  kernel re-derives the segment words' constants per claim group).
+  kernel re-derives the segment words' constants per claim group);
+* static first claims (claim w to worker wave w) never outnumber the waves or the claims.
 
 Round 2's parity soak found a launch of a few wave-blocks across a 2^24-k boundary
 whose realigned wave-block count left a counter without waves; these cases pin it.
@@ -26,7 +27,8 @@ WPB = 4  # waves per workgroup
 class DiagLaunch(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("k_begin", "k_end", "i_begin", "i_end", "wb_begin", "n_wblocks",
                                                 "n_big", "n_chunks", "worker_blocks")] + \
-               [(n, ctypes.c_uint32) for n in ("chunk", "chunk_tail", "rbits", "wave_block")]
+               [(n, ctypes.c_uint32) for n in ("chunk", "chunk_tail", "rbits", "wave_block")] + \
+               [("n_static", ctypes.c_uint64)]
 
 
 def geometry(nonce, wb, wbits, k0, k1, max_blocks):
@@ -51,6 +53,12 @@ def check(d, max_blocks):
     assert covered >= d.n_wblocks > covered - d.chunk_tail  # the last (tail) claim is the only partial one
     holders = min(d.n_chunks, CLAIM_COUNTERS)
     assert holders <= d.worker_blocks <= max(max_blocks, CLAIM_COUNTERS)
+    # static first claims (the chunk-length-0 template launches below k = 2^24): claim w goes
+    # to worker wave w, so there are at most as many as waves, and the counters hand out the
+    # rest -- every counter holding one of those still has a workgroup (holders above)
+    assert d.n_static <= min(d.n_chunks, d.worker_blocks * WPB)
+    if d.k_begin >= (1 << 24):
+        assert d.n_static == 0
     # no more workgroups than the claims need (one wave per claim, rounded up to a workgroup)
     assert d.worker_blocks <= max(-(-d.n_chunks // WPB), holders)
     # a launch spanning chunk lengths 1..3 (plan.cpp lspan): no claim straddles k = 256 or

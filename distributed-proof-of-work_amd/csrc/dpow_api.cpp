@@ -480,7 +480,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         uint64_t worker_blocks = 0;
         rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), &worker_blocks,
                          c->min_chunk_override ? c->min_chunk_override : launch_min_chunk(ntz, L.rbits),
-                         c->cpw_override ? c->cpw_override : kClaimsPerWave);
+                         c->cpw_override ? c->cpw_override : launch_claims_per_wave(ntz, L.rbits));
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.poll_wb = c->poll_override ? c->poll_override : launch_poll_wb(ntz, L.rbits);

@@ -312,6 +312,10 @@ uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits) {
     return expect <= kFastPollCands ? kFastPollWb : slow;
 }
 
+uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits) {
+    return expected_first_hit(ntz, rbits) <= kFastPollCands ? kShortClaimsPerWave : kClaimsPerWave;
+}
+
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits) {
     return DPOW_SMALL_GRIDS && expected_first_hit(ntz, rbits) <= kTinyExpect ? kTinyChunk : kMinChunk;
 }

@@ -128,6 +128,12 @@ constexpr uint64_t kTinyExpect = 1ull << 21;
 constexpr uint64_t kMidExpect = 1ull << 26;
 constexpr uint64_t kTinyChunk = 2;
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits);
+// Claims per wave (chunk sizing) of a search expected to end within kFastPollCands
+// candidates: 64 (smaller chunks), else kClaimsPerWave.  A rank that another rank's hit stops
+// must finish every chunk below it, so the chunk sets its drain: an 8-GPU rank's stop at
+// N = 8 186 -> 139 us, its owner's search 2.510 -> 2.517 ms (profiles/r03_cpw_probe.json).
+constexpr uint64_t kShortClaimsPerWave = 64;
+uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits);
 
 // Worker workgroups per CU for one launch (before the device share).  The full
 // persistent grid (kMaxBlocksPerCu = 6) has the highest rate, but a launch that is

@@ -2,7 +2,7 @@
 //
 // dpow_search replaces the reference miner's enumeration loop
 // (worker.go:301-400): plan the window into launches (plan.cpp), queue them on
-// the context's stream behind one reset kernel with at most kDepth in flight,
+// the context's stream (behind the k = 0 kernel when the window holds k = 0) with at most kDepth in flight,
 // and re-verify a hit with the host MD5 before returning it.  Each launch's
 // last retiring workgroup writes a completion record (the control block as of
 // the end of the launch) to pinned host memory; the host polls that record rather
@@ -805,7 +805,7 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
     PlannedLaunch pl;
     size_t n = 0;
     while (planner.next(pl)) {
-        if (pl.k0) continue;  // k = 0: the search's start kernel, not an md5 launch
+        if (pl.k0) continue;  // k = 0: the search's k = 0 kernel, not an md5 launch
         uint64_t wblocks = 0;
         const int r = size_launch(pl, max_blocks, ~0ull, &wblocks);
         if (r < 0) return set_error(r, "dpow_diag_launch_geometry: launch grid leaves a claim counter without waves");

@@ -710,7 +710,7 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 // memory, mapped), it relays the node's Found fan-out the same way: a lower best of
 // another rank goes to Ctrl::best (atomicMin) -- the waves stop at it at their next
 // group -- and a raised node stop stops the launch.  The host injecting the same best
-// through a kernel on a second stream took 50-160 us to start that kernel beside the
+// through a kernel on a second stream (round 2's dpow_search_bound) took 50-160 us to start that kernel beside the
 // running grid (profiles/r03_stop_latency.json).
 //
 // The bound injected by dpow_search_bound (a pinned host word) is relayed the same way.

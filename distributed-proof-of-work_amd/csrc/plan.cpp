@@ -128,7 +128,7 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     const uint32_t L = chunk_len_of(k);
     const uint32_t nblk = nblk_of(L);
     pl.k0 = DPOW_START_K0 && k == 0;
-    // (the start kernel hashes k = 0 from the real chunk-length-0 template: no deltas)
+    // (the k = 0 kernel hashes k = 0 from the real chunk-length-0 template: no deltas)
     uint32_t L_last = L;
     if (!pl.k0 && k >= 1 && lseg_template(k)) {
         // Merge the following chunk lengths (up to 3) with the same block count.

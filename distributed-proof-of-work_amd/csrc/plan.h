@@ -14,7 +14,7 @@ struct PlannedLaunch {
     dpow_plan_launch info;
     Launch L;  // ctrl / cancel / claim / chunk / done_target filled at launch time
     // k = 0 (the chunk of zero bytes, msg = nonce || threadByte): hashed by the search's
-    // start kernel (search_ctrl.hip), not by an md5 launch; L.iv / L.T hold its message.
+    // k = 0 kernel (search_ctrl.hip), not by an md5 launch; L.iv / L.T hold its message.
     bool k0 = false;
 };
 
@@ -28,7 +28,7 @@ uint64_t word2_period(uint32_t sh);
 constexpr uint64_t kLspanMaxExpect = 1ull << 28;
 uint64_t lspan_end(size_t nonce_len, uint32_t rbits, uint32_t ntz);
 #ifndef DPOW_START_K0
-#define DPOW_START_K0 1  // k = 0 hashed by the search's start kernel (A/B switch)
+#define DPOW_START_K0 1  // k = 0 hashed by the search's k = 0 kernel (A/B switch)
 #endif
 #ifndef DPOW_STATIC_FIRST_HOST
 #define DPOW_STATIC_FIRST_HOST 1  // static first claims in the "_ls" kernels (A/B switch; the kernels'

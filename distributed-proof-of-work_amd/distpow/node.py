@@ -50,7 +50,7 @@ def owner_rank(global_idx: int, world: int) -> int:
 
 
 RANK_RATE = 2.17e11        # candidates/s of one MI355X on the one-block layouts (bench `value`)
-# node_mine's fixed cost per batch c: the window's search call (start kernel, launch, drain,
+# node_mine's fixed cost per batch c: the window's search call (launch, drain,
 # completion record) plus the batch boundary (pinned copy in, all-reduce MIN, copy out,
 # synchronize).  Measured on an MI355X over a world-1 RCCL group (tests/test_gpu_rccl.py,
 # bench.py `collective`): boundary 31-33 us, a whole batch of 2^16 candidates 74-80 us.

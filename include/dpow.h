@@ -184,7 +184,7 @@ typedef struct dpow_plan_launch {
     uint32_t w0, sh;           /* variable bytes start at word w0, byte shift sh */
     uint32_t chunk_len;        /* L: chunk bytes of k_begin ... */
     uint32_t chunk_len_last;   /* ... and of k_end - 1 (one launch may span chunk lengths 1..3) */
-    uint32_t start_kernel;     /* 1: k = 0, hashed by the search's start kernel, not an md5 launch */
+    uint32_t start_kernel;     /* 1: k = 0, hashed by the search's k = 0 kernel, not an md5 launch */
 } dpow_plan_launch;
 int dpow_plan_window(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
                      uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,

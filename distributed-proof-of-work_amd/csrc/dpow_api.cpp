@@ -88,8 +88,8 @@ constexpr size_t kStaleWord = 8;
 constexpr size_t kBoundWord = 16;  // uint32 index of an 8-byte-aligned 64-bit word
 constexpr size_t kCancelPage = 128;
 // Completion-record wait: spin for the first kSpinNs of a search (time-to-secret),
-// then poll at kPollNs (20 us in round 2: a record waited up to that long to be seen,
-// profiles/r03_stop_latency.json; the thread sleeps between polls either way).
+// then poll at kPollNs (20 us in round 2: a record waited up to that long to be seen once
+// a search ran past the spin; the thread sleeps between polls either way).
 constexpr int64_t kSpinNs = 200000;
 constexpr long kPollNs = 5000;
 constexpr int64_t kNoDeadline = INT64_MAX;

@@ -36,7 +36,8 @@
 // (Launch::seg0 == kLsegBase): the pad word W0 + 1 and the bit-length word are segment
 // words.  0: every other launch.  Separate kernels, in their own namespace: holding the
 // bit-length word's K + M in VGPRs cost the sweep kernel 2 % through register assignment
-// alone, with an identical instruction count (217.3 -> 214.0 GH/s, profiles/r03_ab_lspan.log).
+// alone, with an identical instruction count (217.3 -> 214.0 GH/s in an A/B early in round 3;
+// that log did not survive the session).
 #ifndef DPOW_VLS
 #define DPOW_VLS 0
 #endif
@@ -711,7 +712,8 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 // another rank goes to Ctrl::best (atomicMin) -- the waves stop at it at their next
 // group -- and a raised node stop stops the launch.  The host injecting the same best
 // through a kernel on a second stream (round 2's dpow_search_bound) took 50-160 us to start that kernel beside the
-// running grid (profiles/r03_stop_latency.json).
+// running grid (measured early in round 3 with a stop-latency probe whose log did not survive;
+// tools/small_search_probe.py --stop measures the stop as it is now).
 //
 // The bound injected by dpow_search_bound (a pinned host word) is relayed the same way.
 //

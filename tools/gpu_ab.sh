@@ -1,5 +1,5 @@
 # A/B of prebuilt libraries (tools/ab_variants.py) through gpurun:
-#   gpurun --timeout 900 -- bash tools/gpu_ab3.sh <tag> lib1.so lib2.so ...
+#   gpurun --timeout 900 -- bash tools/gpu_ab.sh <tag> lib1.so lib2.so ...
 set -o pipefail
 tag=$1; shift
 mkdir -p gpurun_out/$tag

@@ -671,11 +671,11 @@ DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_
 // It also resets the next search's control block (ctrl_next): every launch of this search
 // runs before any of the next one's (stream order), so the next search needs no reset
 // kernel in front of its first launch.
-// (The two-block kernels pass ctrl_next = null and publish() derives it from ctrl -- the
-// ring is kCtrlRing * 128 bytes, aligned to its size: one more pointer live across their
-// hash loop, which sits at the SGPR limit, put SGPR spill reloads into it.  The one-block
-// kernels pass it: deriving it there moved the sweep kernel's register assignment and cost
-// it 0.6 % (218.1 -> 216.8 GH/s, profiles/r03_ab_publish.log).)
+// (Some two-block kernels pass ctrl_next = null and publish() derives it from ctrl -- the
+// ring is kCtrlRing * 128 bytes, aligned to its size -- where that keeps SGPR spill reloads
+// out of their hash loop (kLaunchPoll).  The one-block kernels pass it: deriving it there
+// moved the sweep kernel's register assignment and cost it 0.6 % (218.1 -> 216.8 GH/s,
+// profiles/r03_ab_publish.log).)
 __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim,
                                                   Ctrl *ctrl_next) {
     if (ctrl_next == nullptr) {
@@ -871,6 +871,17 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
 template <int NBLK, int W0>
 constexpr bool kLongSgpr = NBLK == 2 || W0 >= DPOW_SGPR_LONG_W0;
 
+// Whether a kernel reads the poll group (Launch::poll_wb) and the next search's control block
+// (Launch::ctrl_next) from the launch, or uses the compile-time group and derives the block in
+// publish().  The two-block kernels sit at their SGPR budget, and which choice leaves their hash
+// loop free of SGPR spill reloads depends on the layout's register assignment, not on the count
+// of live values (tools/isa_loop.py over all four combinations; the two flags chosen alike
+// leave every two-block layout at 0-1 reloads per wave-block except <2,12,0> (4 in every
+// combination) and <2,15,0> / <2,15,3> (3); one reload-heavy choice for all of them cost 3-4 %
+// at <2,14,1>, <2,14,3>, <2,15,1> against round 2's build in a same-box A/B).
+template <int NBLK, int W0, int SH>
+constexpr bool kLaunchPoll = NBLK == 1 || SH == 1 || SH == 2 || (SH == 0 && W0 == 15) || (SH == 3 && W0 >= 14);
+
 template <int NBLK, int W0, int SH, bool EQ>
 DPOW_DEV void search_body(const Launch &L) {
     if (blockIdx.x == 0) {  // dispatched first: the watcher
@@ -1002,9 +1013,8 @@ DPOW_DEV void search_body(const Launch &L) {
         // Down-counters keep the loop's live SGPRs at a plain loop's count.
         uint64_t i0 = i_first;
         uint32_t left = nb;
-        // (two final blocks: the compile-time group -- a runtime one kept one more SGPR live
-        // across the hash loop, where their K + M constants already fill the budget)
-        const uint32_t poll_wb = NBLK == 2 ? (uint32_t)DPOW_POLL_WB : L.poll_wb;
+        // (some two-block layouts: the compile-time group, kLaunchPoll)
+        const uint32_t poll_wb = kLaunchPoll<NBLK, W0, SH> ? L.poll_wb : (uint32_t)DPOW_POLL_WB;
         for (;;) {
             uint32_t q = left < poll_wb ? left : poll_wb;
 #if DPOW_SPAN
@@ -1099,7 +1109,7 @@ DPOW_DEV void search_body(const Launch &L) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, NBLK == 2 ? nullptr : L.ctrl_next);
+        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
     }
 }
 

@@ -71,6 +71,9 @@ namespace DPOW_KNS {
 #ifndef DPOW_NUM_SGPR_LONG
 #define DPOW_NUM_SGPR_LONG 96  // long-nonce and two-block layouts (kNumSgpr below)
 #endif
+#ifndef DPOW_NUM_SGPR_W15
+#define DPOW_NUM_SGPR_W15 100  // two-block layouts at W0 = 15 (kW15Sgpr below)
+#endif
 #ifndef DPOW_SGPR_LONG_W0
 #define DPOW_SGPR_LONG_W0 8
 #endif
@@ -866,10 +869,15 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
 // and two final blocks -- get 96: at 72 the compiler spills them to VGPR lanes
 // and reloads each with a v_readlane in every wave-block (tools/isa_loop.py:
 // 4-41 per wave-block; 0 at 96).
-// (The attribute takes no template-dependent value: two kernel templates share
-// one body, and md5_variant.hip instantiates the one kLongSgpr selects.)
+// The two-block W0 = 15 layouts get 100 (DPOW_NUM_SGPR_W15): at 96 three of them kept 3
+// spill reloads per wave-block in every launch-field choice (kLaunchPoll), at 100 they keep
+// 0-1; for the other two-block layouts 100 is no better than 96.  7 waves still fit.
+// (The attribute takes no template-dependent value: three kernel templates share
+// one body, and md5_variant.hip instantiates the one kLongSgpr / kW15Sgpr select.)
 template <int NBLK, int W0>
 constexpr bool kLongSgpr = NBLK == 2 || W0 >= DPOW_SGPR_LONG_W0;
+template <int NBLK, int W0>
+constexpr bool kW15Sgpr = NBLK == 2 && W0 == 15;
 
 // Whether a kernel reads the poll group (Launch::poll_wb) and the next search's control block
 // (Launch::ctrl_next) from the launch, or uses the compile-time group and derives the block in
@@ -1122,6 +1130,12 @@ md5_search_kernel(const Launch L) {
 template <int NBLK, int W0, int SH, bool EQ>
 __global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR_LONG)))
 md5_search_kernel_lsgpr(const Launch L) {
+    search_body<NBLK, W0, SH, EQ>(L);
+}
+
+template <int NBLK, int W0, int SH, bool EQ>
+__global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR_W15)))
+md5_search_kernel_w15sgpr(const Launch L) {
     search_body<NBLK, W0, SH, EQ>(L);
 }
 

@@ -34,7 +34,7 @@ def disasm(csrc, nblk, sh, extra):
 
 
 def kernel_lines(text, nblk, w0, sh, eq=0):
-    pat = re.compile(rf"md5_search_kernel(?:_lsgpr)?ILi{nblk}ELi{w0}ELi{sh}ELb{eq}E.*>:")
+    pat = re.compile(rf"md5_search_kernel(?:_lsgpr|_w15sgpr)?ILi{nblk}ELi{w0}ELi{sh}ELb{eq}E.*>:")
     out, on = [], False
     for line in text.splitlines():
         if pat.search(line):

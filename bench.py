@@ -4,6 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+With --gpus N > 1 and no launcher (WORLD_SIZE unset), bench.py starts the N ranks itself
+(a child torch.distributed.run on 127.0.0.1) and relays rank 0's line; a WORLD_SIZE that
+differs from --gpus is an error.
+
 A step is one batch of the hot path: every rank searches its prefix partition
 (worker_byte = rank, worker_bits = log2 N; coordinator.go:127,326) over the same
 k-window holding 2^36 candidates per GPU (nonce
@@ -38,7 +42,6 @@ SWEEP_NTZ = 32
 CANDIDATES_PER_GPU_PER_STEP = 1 << 36
 STRONG_TOTAL_PER_STEP = 1 << 38    # --strong: fixed total work per step
 K0 = 1 << 24                      # start of the L = 4 segment
-PROFILE_TAG = "r03"                # profiles/<tag>_summary.json of the current kernel
 # time-to-secret at N > 1: node_mine's constant per-rank batch sized for N and the node (node.auto_batch_candidates)
 TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first_ms: the first, cold)
 # N > 1 time-to-secret: node_mine (batch-synchronous, RCCL all-reduce at batch boundaries,
@@ -77,13 +80,24 @@ def main():
                     help="N = 1 without a (world-1) process group: no collective in the step")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank searches on device 0 (with --backend gloo)")
+    ap.add_argument("--print-launch", action="store_true",
+                    help="print the rank launcher's command (--gpus N > 1 without WORLD_SIZE) as JSON and exit")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # No launcher around us: start the N ranks ourselves (one process per GPU), as a child
+        # process -- nothing here has touched the GPU yet -- and relay rank 0's line.
+        sys.exit(launch_ranks(args))
+    if args.print_launch:
+        print(json.dumps({"launch": None, "world_size": int(env_world or "1")}))
+        return
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the command line disagree")
+        sys.exit(2)
     device = 0 if args.same_device else local_rank
     torch.cuda.set_device(device)
     tick_group = None
@@ -123,7 +137,14 @@ def main():
     per_gpu = (STRONG_TOTAL_PER_STEP // world) if args.strong else CANDIDATES_PER_GPU_PER_STEP
     batch_k = per_gpu // R  # same k-window on every rank
 
+    # dpow_open: the first one in the process loads every search kernel on the device
+    # ("Search start"); a second one does not
+    t_open = time.perf_counter()
     miner = distpow.Miner(device)
+    open_ms = [(time.perf_counter() - t_open) * 1e3]
+    t_open = time.perf_counter()
+    distpow.Miner(device).close()
+    open_ms.append((time.perf_counter() - t_open) * 1e3)
     dev = torch.device("cuda", device) if args.backend == "nccl" else torch.device("cpu")
     red = torch.empty(2, dtype=torch.int64, device=dev)
 
@@ -246,14 +267,18 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_threads, args.cpu_seconds)
 
-    # Memory traffic per sweep launch from the committed rocprofv3 PMC passes of this kernel
-    # (FETCH_SIZE and WRITE_SIZE in separate passes, tools/profile_gpu.sh + tools/summarize_profile.py),
-    # uncorrected: the search reads no data, so these bytes are kernarg scalar loads, the claim
-    # atomics and the completion records -- not algorithmic HBM traffic (that is 0 per candidate).
-    traffic, traffic_src, issue = None, None, None
-    prof = os.path.join(ROOT, "profiles", PROFILE_TAG + "_summary.json")
-    if os.path.exists(prof):
-        ps = json.load(open(prof))
+    # Memory traffic and the PMC issue model per sweep launch, from the committed rocprofv3
+    # summary (tools/profile_gpu.sh + tools/summarize_profile.py) of THIS build: the
+    # profiles/*_summary.json whose build_id is distpow.build_id(); none -> null, with the
+    # reason.  Traffic is uncorrected: the search reads no data, so these bytes are kernarg
+    # scalar loads, the claim atomics and the completion records -- not algorithmic HBM
+    # traffic (that is 0 per candidate).
+    traffic, traffic_src, issue, prof_reason = None, None, None, None
+    ps, prof = profile_summary_of(distpow.build_id())
+    if ps is None:
+        prof_reason = (f"no profiles/*_summary.json was taken of build {distpow.build_id()} (the benched one): "
+                       "traffic and the PMC issue model are not quoted from another build")
+    else:
         if "valu_busy_issue_model" in ps:
             # SQ_INSTS_VALU per SIMD-cycle weighted by the hash block's mix (2 cycles per
             # full-rate, 4 per half-rate wave64 instruction): ~1.0 = the SIMDs issue VALU
@@ -261,12 +286,15 @@ def main():
             issue = {"valu_busy": round(ps["valu_busy_issue_model"], 4),
                      "valu_insts_per_candidate": round(ps["valu_insts_per_candidate"], 2),
                      "clock_ghz": round(ps["effective_clock_ghz"], 3),
-                     "source": f"profiles/{PROFILE_TAG}_summary.json (rocprofv3 SQ/GRBM pass)"}
+                     "source": f"{prof} (rocprofv3 SQ/GRBM pass, build {ps['build_id']})"}
         if "hbm_bytes_per_launch" in ps:
             traffic = int(ps["hbm_bytes_per_launch"])
-            traffic_src = (f"profiles/{PROFILE_TAG}_summary.json: FETCH_SIZE + WRITE_SIZE per "
+            traffic_src = (f"{prof} (build {ps['build_id']}): FETCH_SIZE + WRITE_SIZE per "
                            f"{ps.get('candidates_per_sweep_launch', 0)}-candidate launch, uncorrected; "
                            "claim atomics + kernarg loads, no algorithmic HBM bytes")
+    # The box's shader clock under full VALU load, from this run's issue-rate probe: frac is
+    # priced at the 2.4 GHz spec clock, and boxes run 2.30-2.36 GHz under this load.
+    box_clk = (probe.get("md5_step_mix") or {}).get("clock_ghz")
 
     if rank == 0:
         cus, bpc, tpb = miner.geometry()
@@ -307,8 +335,14 @@ def main():
                 "candidates_per_launch": int(cand_per_launch),
                 "launches": int(st.launches),
                 "issue": issue,
+                "profile_reason": prof_reason,
+                "box_clock_ghz": box_clk,
+                "box_clock_source": "dpow_diag_valu_rate md5_step_mix probe of this run (all CUs busy)" if box_clk else None,
+                "frac_at_box_clock": (round(achieved_tops / (256 * 4 * 32 * box_clk * 1e9 / 1e12), 4)
+                                      if box_clk else None),
             },
             "stream_event_ms": round(stream_ms, 3),
+            "dpow_open_ms": {"first": round(open_ms[0], 3), "again": round(open_ms[1], 3)},
             "valu_probe": probe,
             "time_to_secret": tts,
             "time_to_secret_node_search": ("one rank: Miner.mine" if world == 1 else
@@ -326,6 +360,83 @@ def main():
         board.close()
     if dist_on:
         dist.destroy_process_group()
+
+
+def profile_summary_of(build):
+    """(summary, path) of the committed rocprofv3 summary of `build` (profiles/*_summary.json
+    carrying that build_id; the latest by name when several), or (None, None)."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            ps = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if ps.get("build_id") == build:
+            best = (ps, os.path.relpath(p, ROOT))
+    return best or (None, None)
+
+
+def launcher_argv(argv, nproc, port):
+    """The rank launcher bench.py starts for --gpus N > 1 when no launcher set WORLD_SIZE: the
+    driver's own form (torch.distributed.run, one node, N processes, rendezvous on
+    127.0.0.1), re-running this script with the same arguments."""
+    argv = [a for a in argv if a != "--print-launch"]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: run the N ranks as a child torch.distributed.run (the
+    reference coordinator starts its workers' searches itself, coordinator.go:179-199),
+    relay rank 0's JSON line to stdout and return the child's exit code.  Never re-execs:
+    the child is a separate process, started before this process touches the GPU."""
+    import signal
+    import subprocess
+    cmd = launcher_argv(sys.argv[1:], args.gpus, free_port())
+    if args.print_launch:
+        print(json.dumps({"launch": cmd, "world_size": args.gpus}))
+        return 0
+    if not args.same_device:
+        ndev = torch.cuda.device_count()  # counts devices without initialising them
+        if ndev < args.gpus:
+            log(f"error: --gpus {args.gpus} but {ndev} GPU(s) visible (--same-device rehearses N ranks on one)")
+            return 2
+    log("bench: starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    relay = lambda sig, frame: child.send_signal(sig)  # noqa: E731
+    old = {sg: signal.signal(sg, relay) for sg in (signal.SIGTERM, signal.SIGINT)}
+    lines = 0
+    try:
+        for line in child.stdout:
+            rec = None
+            try:
+                rec = json.loads(line)
+            except ValueError:
+                pass
+            if isinstance(rec, dict) and "metric" in rec:  # rank 0's result line
+                print(line.rstrip("\n"), flush=True)
+                lines += 1
+            else:
+                sys.stderr.write(line)
+        rc = child.wait()
+    finally:
+        for sg, h in old.items():
+            signal.signal(sg, h)
+        if child.poll() is None:
+            child.kill()
+            child.wait()
+    if rc == 0 and lines != 1:
+        log(f"error: the {args.gpus} ranks exited 0 but printed {lines} result lines")
+        return 1
+    return rc
 
 
 def collective_probe(miner, rank, world, dev, board, backend, reps=200):

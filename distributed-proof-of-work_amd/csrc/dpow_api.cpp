@@ -187,11 +187,10 @@ struct dpow_ctx {
     // search waits for its records.
     dpow_node_slot *node = nullptr;
     dpow_node_slot *d_node = nullptr;  // its device alias (the watcher polls it)
-    std::vector<void *> registered;    // host pages registered for the node slots attached so far
-    uint32_t poll_override = 0;  // DPOW_DIAG_POLL_WB (A/B runs): wave-blocks per poll group for every launch
-    uint32_t bpc_override = 0;   // DPOW_DIAG_BPC: worker workgroups per CU for every launch
-    uint32_t min_chunk_override = 0;  // DPOW_DIAG_MIN_CHUNK: minimum wave-blocks per claim (a power of two)
-    uint32_t cpw_override = 0;   // DPOW_DIAG_CPW: big claims per wave (chunk sizing)
+    // A/B overrides of the launch policy (dpow_diag.h): DPOW_DIAG_POLL_WB (wave-blocks per poll
+    // group), DPOW_DIAG_BPC (worker workgroups per CU), DPOW_DIAG_MIN_CHUNK (minimum wave-blocks
+    // per claim, a power of two), DPOW_DIAG_CPW (big claims per wave); 0 = the policy.
+    LaunchKnobs knobs;
     int64_t diag_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // the last search's host timeline (dpow_diag_search_times)
 };
 
@@ -475,15 +474,10 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         Launch &L = pl.L;
         // This search's share of the device's resident workgroups (1 / searches in flight on it).
         const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
-        const uint64_t bpc = c->bpc_override ? c->bpc_override : launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
-        const uint64_t max_blocks = std::max<uint64_t>((uint64_t)c->cus * bpc / share, kClaimCounters);
         uint64_t worker_blocks = 0;
-        rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), &worker_blocks,
-                         c->min_chunk_override ? c->min_chunk_override : launch_min_chunk(ntz, L.rbits),
-                         c->cpw_override ? c->cpw_override : launch_claims_per_wave(ntz, L.rbits));
+        rc = size_search_launch(pl, ntz, c->cus, share, c->knobs, &worker_blocks);
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
-        L.poll_wb = c->poll_override ? c->poll_override : launch_poll_wb(ntz, L.rbits);
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
         L.done_target = done_target;
         L.ctrl = ctrl;
@@ -532,6 +526,68 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     return status;
 }
 
+// Host pages registered for node slots (hipHostRegister: process-wide, not per context).  A
+// context that attaches a slot holds its pages until dpow_close (detaching keeps them, so
+// node_mine's attach / detach per node search costs no registration); a page is registered by
+// its first holder and unregistered when its last holder closes, so two contexts of one
+// process attached to one slot (one per GPU, or the 2-rank rehearsal) never see the page
+// unregistered under a running watcher.  Memory about to be unmapped is released explicitly
+// (dpow_node_release: NodeBoard.close), so a new mapping at the same address is registered
+// afresh instead of reusing the old registration's device alias.
+struct PageEntry {
+    void *page;
+    bool foreign;                    // registered outside this library: never unregistered here
+    std::vector<dpow_ctx *> holders;
+};
+std::mutex g_page_mu;
+std::vector<PageEntry> g_pages;
+
+// A reference of ctx on `page` (registering it if no context holds it).  g_page_mu held.
+hipError_t page_hold_locked(dpow_ctx *c, void *page) {
+    for (PageEntry &pe : g_pages)
+        if (pe.page == page) {
+            if (std::find(pe.holders.begin(), pe.holders.end(), c) == pe.holders.end()) pe.holders.push_back(c);
+            return hipSuccess;
+        }
+    hipError_t e = hipHostRegister(page, 4096, hipHostRegisterMapped);
+    bool foreign = false;
+    if (e == hipErrorHostMemoryAlreadyRegistered) {
+        (void)hipGetLastError();
+        e = hipSuccess;
+        foreign = true;
+    }
+    if (e != hipSuccess) return e;
+    g_pages.push_back(PageEntry{page, foreign, {c}});
+    return hipSuccess;
+}
+
+// Drop entry i (every holder's streams drained by the caller).  g_page_mu held.
+void page_drop_locked(size_t i) {
+    if (!g_pages[i].foreign) (void)hipHostUnregister(g_pages[i].page);
+    g_pages.erase(g_pages.begin() + (long)i);
+}
+
+// dpow_close: ctx's references go (its stream has drained); pages without holders are unregistered.
+void pages_release_ctx(dpow_ctx *c) {
+    std::lock_guard<std::mutex> g(g_page_mu);
+    for (size_t i = g_pages.size(); i-- > 0;) {
+        auto &h = g_pages[i].holders;
+        h.erase(std::remove(h.begin(), h.end(), c), h.end());
+        if (h.empty()) page_drop_locked(i);
+    }
+}
+
+// Kernels loaded per device in this process (search_prepare): once, under a lock.
+hipError_t prepare_device(int device) {
+    static std::mutex mu;
+    static bool prepared[kMaxDevices] = {};
+    std::lock_guard<std::mutex> g(mu);
+    if (device < kMaxDevices && prepared[device]) return hipSuccess;
+    const hipError_t e = search_prepare();
+    if (e == hipSuccess && device < kMaxDevices) prepared[device] = true;
+    return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -565,12 +621,12 @@ int dpow_open(int device, dpow_ctx **out) {
         return hip_fail(e, "hipGetDeviceProperties");
     }
     c->cus = (uint32_t)prop.multiProcessorCount;
-    if (const char *pw = getenv("DPOW_DIAG_POLL_WB")) c->poll_override = (uint32_t)std::max(0, atoi(pw));
-    if (const char *pw = getenv("DPOW_DIAG_BPC")) c->bpc_override = (uint32_t)std::max(0, atoi(pw));
-    if (const char *pw = getenv("DPOW_DIAG_CPW")) c->cpw_override = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_POLL_WB")) c->knobs.poll_wb = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_BPC")) c->knobs.bpc = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_CPW")) c->knobs.cpw = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_MIN_CHUNK")) {
         const uint32_t v = (uint32_t)std::max(0, atoi(pw));
-        if (v && !(v & (v - 1))) c->min_chunk_override = v;
+        if (v && !(v & (v - 1))) c->knobs.min_chunk = v;
     }
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&c->d_ctrl_alloc, 2 * kCtrlRing * kCtrlStride * sizeof(Ctrl))) != hipSuccess ||
@@ -601,6 +657,13 @@ int dpow_open(int device, dpow_ctx **out) {
         dpow_close(c);
         return hip_fail(e, "dpow_open: control state");
     }
+    // Every search kernel resolved on this device before the first search (once per device and
+    // process): a translation unit's code object loads on its first use, which cost round 3's
+    // first search ~1 ms (the k = 0 kernel, then a 972.8 us gap before the "_ls" md5 launch).
+    if ((e = prepare_device(device)) != hipSuccess) {
+        dpow_close(c);
+        return hip_fail(e, "dpow_open: loading the search kernels");
+    }
     *out = c;
     return 0;
 }
@@ -614,7 +677,8 @@ void dpow_close(dpow_ctx *c) {
     if (c->h_snap) (void)hipHostFree(c->h_snap);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    for (void *p : c->registered) (void)hipHostUnregister(p);
+    c->node = c->d_node = nullptr;
+    pages_release_ctx(c);  // after the stream drained: no watcher of ours reads the pages any more
     delete c;
 }
 
@@ -650,26 +714,51 @@ int dpow_search_bound(dpow_ctx *c, uint64_t global_idx) {
 
 int dpow_node_attach(dpow_ctx *c, dpow_node_slot *slot) {
     if (!c) return set_error(DPOW_EINVAL, "dpow_node_attach: ctx is NULL");
-    if (!slot) {
+    if (!slot) {  // detach: the pages stay held (registered) until dpow_close or dpow_node_release
         c->node = c->d_node = nullptr;
         return 0;
     }
     if (((uintptr_t)slot & 7u) != 0u) return set_error(DPOW_EINVAL, "dpow_node_attach: slot not 8-byte aligned");
-    // Map the slot's host page(s) for the watcher (fine-grained: hipHostRegister's
-    // default), once per page per context; unregistered at dpow_close.
+    // Map the slot's host page(s) for the watcher (fine-grained: hipHostRegister's default).
     DPOW_HIP(hipSetDevice(c->device));
     const uintptr_t pg = 4096;
-    for (uintptr_t a = (uintptr_t)slot & ~(pg - 1); a < (uintptr_t)slot + sizeof(dpow_node_slot); a += pg) {
-        void *p = (void *)a;
-        if (std::find(c->registered.begin(), c->registered.end(), p) != c->registered.end()) continue;
-        const hipError_t e = hipHostRegister(p, pg, hipHostRegisterMapped);
-        if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) return hip_fail(e, "dpow_node_attach: hipHostRegister");
-        if (e == hipSuccess) c->registered.push_back(p);
+    {
+        std::lock_guard<std::mutex> g(g_page_mu);
+        for (uintptr_t a = (uintptr_t)slot & ~(pg - 1); a < (uintptr_t)slot + sizeof(dpow_node_slot); a += pg) {
+            const hipError_t e = page_hold_locked(c, (void *)a);
+            if (e != hipSuccess) return hip_fail(e, "dpow_node_attach: hipHostRegister");
+        }
     }
     void *d = nullptr;
     DPOW_HIP(hipHostGetDevicePointer(&d, slot, 0));
     c->node = slot;
     c->d_node = (dpow_node_slot *)d;
+    return 0;
+}
+
+int dpow_node_release(void *mem, size_t len) {
+    if (!mem || !len) return 0;
+    const uintptr_t pg = 4096;
+    const uintptr_t lo = (uintptr_t)mem & ~(pg - 1), hi = (uintptr_t)mem + len;
+    std::lock_guard<std::mutex> g(g_page_mu);
+    for (const PageEntry &pe : g_pages) {
+        const uintptr_t p = (uintptr_t)pe.page;
+        if (p < lo || p >= hi) continue;
+        for (dpow_ctx *h : pe.holders)
+            if (h->node && (uintptr_t)h->node < p + pg && (uintptr_t)h->node + sizeof(dpow_node_slot) > p)
+                return set_error(DPOW_EINVAL, "dpow_node_release: a context is still attached to a slot in the range");
+    }
+    for (size_t i = g_pages.size(); i-- > 0;) {
+        const uintptr_t p = (uintptr_t)g_pages[i].page;
+        if (p < lo || p >= hi) continue;
+        // launches a holder left queued behind its last search may still read the page
+        for (dpow_ctx *h : g_pages[i].holders) {
+            (void)hipSetDevice(h->device);
+            const hipError_t e = hipStreamSynchronize(h->stream);
+            if (e != hipSuccess) return hip_fail(e, "dpow_node_release: hipStreamSynchronize");
+        }
+        page_drop_locked(i);
+    }
     return 0;
 }
 
@@ -796,18 +885,19 @@ int dpow_plan_candidate(const uint8_t *nonce, size_t nonce_len, uint32_t worker_
     return 0;
 }
 
-int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte, uint32_t worker_bits,
-                              uint64_t k_begin, uint64_t k_end, uint64_t max_blocks, dpow_diag_launch *out,
-                              size_t max_launches) {
+int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
+                              uint32_t worker_bits, uint64_t k_begin, uint64_t k_end, uint32_t cus, uint32_t share,
+                              dpow_diag_launch *out, size_t max_launches) {
+    if (cus == 0 || share == 0) return set_error(DPOW_EINVAL, "dpow_diag_launch_geometry: cus and share must be > 0");
     WindowPlanner planner;
-    const int rc = planner.init(nonce, nonce_len, 0, worker_byte, worker_bits, k_begin, k_end);
+    const int rc = planner.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
     if (rc < 0) return set_error(rc, "dpow_diag_launch_geometry: bad arguments");
     PlannedLaunch pl;
     size_t n = 0;
     while (planner.next(pl)) {
         if (pl.k0) continue;  // k = 0: the search's k = 0 kernel, not an md5 launch
         uint64_t wblocks = 0;
-        const int r = size_launch(pl, max_blocks, ~0ull, &wblocks);
+        const int r = size_search_launch(pl, ntz, cus, share, LaunchKnobs{}, &wblocks);
         if (r < 0) return set_error(r, "dpow_diag_launch_geometry: launch grid leaves a claim counter without waves");
         if (out && n < max_launches) {
             dpow_diag_launch &d = out[n];
@@ -825,6 +915,7 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t w
             d.rbits = pl.L.rbits;
             d.wave_block = kWaveBlock;
             d.n_static = pl.L.n_static;
+            d.poll_wb = pl.L.poll_wb;
         }
         ++n;
     }

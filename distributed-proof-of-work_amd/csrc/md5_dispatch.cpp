@@ -28,4 +28,15 @@ hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu) {
     return hipErrorInvalidValue;
 }
 
+hipError_t search_prepare() {
+    hipError_t e = search_k0_prepare();
+#define DPOW_PREP(n, s) \
+    if (e == hipSuccess) e = variant_prepare_##n##_##s();
+    DPOW_PREP(1, 0) DPOW_PREP(1, 1) DPOW_PREP(1, 2) DPOW_PREP(1, 3)
+    DPOW_PREP(2, 0) DPOW_PREP(2, 1) DPOW_PREP(2, 2) DPOW_PREP(2, 3)
+    DPOW_PREP(1, 0_ls) DPOW_PREP(2, 0_ls)
+#undef DPOW_PREP
+    return e;
+}
+
 }  // namespace dpow

@@ -68,6 +68,20 @@ hipError_t DPOW_NAME(variant_launch_, DPOW_VNBLK, DPOW_VSH)(int w0, const Launch
     return hipGetLastError();
 }
 
+// Resolve every kernel of this translation unit on the current device (dpow_open, once per
+// device and process).  HIP loads a translation unit's code object on the first use of any
+// of its kernels: round 3's first search after dpow_open waited 972.8 us between its k = 0
+// kernel and its first md5 launch, the "_ls" unit's load (profiles/r03_final_tts_timeline.json).
+hipError_t DPOW_NAME(variant_prepare_, DPOW_VNBLK, DPOW_VSH)() {
+    for (const auto &row : kTable)
+        for (KernelFn fn : row) {
+            hipFuncAttributes a;
+            const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(fn));
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
 hipError_t DPOW_NAME(variant_occupancy_, DPOW_VNBLK, DPOW_VSH)(int w0, int *blocks_per_cu) {
     KernelFn fn = pick(w0, false);
     if (!fn) return hipErrorInvalidValue;

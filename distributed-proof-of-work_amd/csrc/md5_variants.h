@@ -9,7 +9,8 @@ namespace dpow {
 
 #define DPOW_DECL_VARIANT(n, s)                                                                  \
     hipError_t variant_launch_##n##_##s(int w0, const Launch &L, uint32_t grid, hipStream_t st); \
-    hipError_t variant_occupancy_##n##_##s(int w0, int *blocks_per_cu);
+    hipError_t variant_occupancy_##n##_##s(int w0, int *blocks_per_cu);                        \
+    hipError_t variant_prepare_##n##_##s();
 DPOW_DECL_VARIANT(1, 0)
 DPOW_DECL_VARIANT(1, 1)
 DPOW_DECL_VARIANT(1, 2)
@@ -35,6 +36,9 @@ inline bool variant_exists(int nblk, int w0, int sh) {
 // completion record.)
 hipError_t search_launch(int nblk, int w0, int sh, const Launch &L, uint32_t grid, hipStream_t stream);
 hipError_t search_occupancy(int nblk, int w0, int sh, int *blocks_per_cu);
+// Load and resolve every search kernel (all layouts, the "_ls" ones, the k = 0 and init
+// kernels) on the current device, so no search pays a code object's first-use load.
+hipError_t search_prepare();
 
 // The k = 0 kernel (search_ctrl.hip): hashes the k = 0 candidates (msg = nonce ||
 // threadByte, R of them) and writes k0.snap's record with their first hit.
@@ -50,6 +54,7 @@ struct StartK0 {
     uint32_t T[32];    // their words, threadByte zeroed (plan.cpp build_template)
 };
 hipError_t search_k0(const StartK0 &k0, hipStream_t stream);
+hipError_t search_k0_prepare();
 // A context's initial control state (search_ctrl.hip): n_ctrl clean control blocks, n_claims
 // zero claim counters.
 hipError_t context_init(Ctrl *ctrl, uint32_t n_ctrl, unsigned long long *claims, uint32_t n_claims,

@@ -15,6 +15,8 @@
 // nonce-only blocks before p are hashed here once (midstate).
 #include "plan.h"
 
+#include <algorithm>
+
 #include <string.h>
 
 #include "md5_host.h"
@@ -318,6 +320,19 @@ uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits) {
 
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits) {
     return DPOW_SMALL_GRIDS && expected_first_hit(ntz, rbits) <= kTinyExpect ? kTinyChunk : kMinChunk;
+}
+
+int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t share, const LaunchKnobs &knobs,
+                       uint64_t *worker_blocks) {
+    Launch &L = pl.L;
+    const uint64_t bpc = knobs.bpc ? knobs.bpc : launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
+    const uint64_t max_blocks = std::max<uint64_t>(cus * bpc / std::max<uint64_t>(share, 1), kClaimCounters);
+    const int rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), worker_blocks,
+                               knobs.min_chunk ? knobs.min_chunk : launch_min_chunk(ntz, L.rbits),
+                               knobs.cpw ? knobs.cpw : launch_claims_per_wave(ntz, L.rbits));
+    if (rc < 0) return rc;
+    L.poll_wb = knobs.poll_wb ? knobs.poll_wb : launch_poll_wb(ntz, L.rbits);
+    return 0;
 }
 
 uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits) {

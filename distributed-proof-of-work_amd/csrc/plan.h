@@ -151,4 +151,16 @@ uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits);
 constexpr uint64_t kMaxBlocksPerCu = DPOW_BLOCKS_PER_CU;
 uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits);
 
+// The whole sizing of one dpow_search launch, shared by dpow_search and the geometry
+// diagnostic (dpow_diag_launch_geometry), so the diagnostic checks the grids searches run:
+// the device share of cus x launch_blocks_per_cu workgroups (at least one per claim
+// counter), size_launch with the ntz-dependent expected first hit, minimum chunk and
+// claims per wave, and the poll group (L.poll_wb).  Non-zero knobs override the policy
+// (the DPOW_DIAG_* A/B environment of dpow_open).
+struct LaunchKnobs {
+    uint32_t bpc = 0, min_chunk = 0, cpw = 0, poll_wb = 0;
+};
+int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t share, const LaunchKnobs &knobs,
+                       uint64_t *worker_blocks);
+
 }  // namespace dpow

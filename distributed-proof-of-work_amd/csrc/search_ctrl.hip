@@ -96,6 +96,13 @@ hipError_t context_init(Ctrl *ctrl, uint32_t n_ctrl, unsigned long long *claims,
     return hipGetLastError();
 }
 
+hipError_t search_k0_prepare() {
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(search_k0_kernel));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(context_init_kernel));
+    return e;
+}
+
 hipError_t search_k0(const StartK0 &k0, hipStream_t stream) {
     hipLaunchKernelGGL(search_k0_kernel, dim3(1), dim3(kBlockThreads), 0, stream, k0);
     return hipGetLastError();

@@ -18,7 +18,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 INCLUDE = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
 # DPOW_LIB_PATH overrides the in-tree library (A/B builds in tools/ab_variants.py only;
-# such a library is not checked against the source hash).
+# such a library is not checked against the source hash, but its ABI version must be
+# this binding's: check_abi).
 LIB_OVERRIDE = os.environ.get("DPOW_LIB_PATH")
 LIB_PATH = LIB_OVERRIDE or os.path.join(_HERE, "libdpow.so")
 
@@ -123,6 +124,35 @@ def check_build():
                       f"{want!r}: rebuild it (make -C distributed-proof-of-work_amd/csrc)")
 
 
+def header_abi_version(header=None):
+    """DPOW_ABI_VERSION as include/dpow.h of this tree defines it: the ABI this binding's
+    argtypes and structs were written for."""
+    path = header or os.path.join(INCLUDE, "dpow.h")
+    with open(path) as f:
+        m = re.search(r"^#define\s+DPOW_ABI_VERSION\s+(\d+)\s*$", f.read(), re.M)
+    if not m:
+        raise ImportError(f"{path} defines no DPOW_ABI_VERSION")
+    return int(m.group(1))
+
+
+def check_abi(L, path):
+    """Refuse a library built for another ABI (include/dpow.h: a consumer built against
+    another version must refuse it).  dpow_abi_version() is the only entry point called
+    before the check; a library without it is refused too."""
+    want = header_abi_version()
+    fn = getattr(L, "dpow_abi_version", None)
+    if fn is None:
+        raise ImportError(f"{path} exports no dpow_abi_version: not a libdpow.so")
+    fn.restype = ctypes.c_int
+    fn.argtypes = []
+    have = fn()
+    if have != want:
+        raise ImportError(f"{path} implements DPOW_ABI_VERSION {have}, but this binding (include/dpow.h) is "
+                          f"version {want}: refusing it (rebuild the library from this tree, or use the binding "
+                          f"of the tree it was built from)")
+    return have
+
+
 def _preload_torch_hip():
     # torch ships its own libamdhip64 (soname libamdhip64.so.7).  Loading torch
     # first makes libdpow bind to that same runtime instead of a second copy,
@@ -143,6 +173,7 @@ def lib():
         raise ImportError(f"DPOW_LIB_PATH={LIB_PATH} does not exist")
     _preload_torch_hip()
     L = ctypes.CDLL(LIB_PATH)
+    check_abi(L, LIB_PATH)  # every library, the DPOW_LIB_PATH overrides included
     u8p = ctypes.POINTER(ctypes.c_uint8)
     u32p = ctypes.POINTER(ctypes.c_uint32)
     u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -157,6 +188,7 @@ def lib():
         "dpow_search_bound": (ctypes.c_int, [vp, ctypes.c_uint64]),
         "dpow_node_attach": (ctypes.c_int, [vp, vp]),
         "dpow_node_slot_reset": (None, [vp]),
+        "dpow_node_release": (ctypes.c_int, [vp, ctypes.c_size_t]),
         "dpow_node_post": (None, [vp, ctypes.c_uint64]),
         "dpow_node_stop": (None, [vp]),
         "dpow_node_vote": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
@@ -200,9 +232,10 @@ def lib():
         "dpow_worker_trace": (ctypes.c_size_t, [vp, ctypes.c_char_p, ctypes.c_size_t]),
         "dpow_worker_active_tasks": (ctypes.c_int, [vp]),
     }
+    missing = [name for name in sig if not hasattr(L, name)]
+    if missing:  # same ABI version, yet entry points missing: not a library of this ABI either
+        raise ImportError(f"{LIB_PATH} lacks entry points of DPOW_ABI_VERSION {header_abi_version()}: {missing}")
     for name, (res, args) in sig.items():
-        if LIB_OVERRIDE and not hasattr(L, name):
-            continue  # an older A/B build (tools/ab_variants.py) may lack a newer entry point
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

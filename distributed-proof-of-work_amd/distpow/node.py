@@ -173,12 +173,34 @@ class NodeBoard:
         name = [None]
         shm = None
         if rank == 0:
-            shm = shared_memory.SharedMemory(name=f"dpow_node_{os.getpid()}_{uuid.uuid4().hex[:12]}", create=True,
-                                             size=cls.nbytes(world))
-            name[0] = shm.name
+            try:
+                shm = shared_memory.SharedMemory(name=f"dpow_node_{os.getpid()}_{uuid.uuid4().hex[:12]}",
+                                                 create=True, size=cls.nbytes(world))
+                name[0] = shm.name
+            except OSError:  # e.g. /dev/shm full: every rank goes on without a board (name None)
+                name[0] = None
         dist.broadcast_object_list(name, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if name[0] is None:
+            return None
+        ok = [True]
         if rank != 0:
-            shm = shared_memory.SharedMemory(name=name[0])
+            try:
+                shm = shared_memory.SharedMemory(name=name[0])
+                # Rank 0 created it and unlinks it below; an attaching rank's resource tracker
+                # would try to unlink it again at exit (and warn): this rank does not own it.
+                from multiprocessing import resource_tracker
+                resource_tracker.unregister(shm._name, "shared_memory")
+            except OSError:
+                ok[0], shm = False, None
+        # every rank must have it mapped, or none uses it
+        oks = [None] * world
+        dist.all_gather_object(oks, ok[0], group=group)
+        if not all(oks):
+            if shm is not None:
+                shm.close()
+                if rank == 0:
+                    shm.unlink()
+            return None
         board = cls(shm, world, rank)
         if rank == 0:
             for i in range(cls.SLOTS):
@@ -213,7 +235,12 @@ class NodeBoard:
         lib().dpow_node_post(slot, global_idx)
 
     def close(self):
+        """Unmap the board (every rank's context detached first: node_mine detaches at its
+        end); the library drops its HIP registration of the pages (dpow_node_release), so a
+        later board mapped at the same address is registered afresh."""
         if self._shm is not None:
+            from ._lib import check, lib
+            check(lib().dpow_node_release(self._base, self.nbytes(self.world)), "dpow_node_release")
             self._base = 0
             try:
                 self._shm.close()
@@ -231,7 +258,7 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
               batch_k: Optional[int] = None, k_start: int = 0, k_limit: int = DPOW_K_LIMIT, group=None,
               device=None, cancelled: Callable[[], bool] = lambda: False, growth: int = 4,
               batch_k_max: Optional[int] = None, batch_candidates_max: int = 1 << 29,
-              board: Optional[NodeBoard] = None, attach_fn: Callable[[Optional[int]], None] = lambda s: None
+              board: Optional[NodeBoard] = None, attach_fn: Optional[Callable[[Optional[int]], None]] = None
               ) -> NodeResult:
     """Search until the first hit of the whole node (deterministic) or a cancel vote.
 
@@ -258,14 +285,17 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
 
     board / attach_fn: the node's shared-memory Found fan-out (NodeBoard); attach_fn(slot)
     attaches a slot address to this rank's search context (Miner.attach_node), None
-    detaches.
+    detaches.  Without attach_fn the board still carries the vote and the posted hits
+    between batches, but no running kernel sees another rank's hit, so the batch stays the
+    expected-time one (not BOARD_BATCH_CANDIDATES, which relies on the kernels stopping).
     """
     import torch
     import torch.distributed as dist
 
     wb, wbits = partition_of_rank(rank, world)
     if batch_k is None:
-        cand = BOARD_BATCH_CANDIDATES if board is not None else auto_batch_candidates(num_trailing_zeros, world)
+        cand = (BOARD_BATCH_CANDIDATES if board is not None and attach_fn is not None
+                else auto_batch_candidates(num_trailing_zeros, world))
         batch_k = max(1, cand >> (8 - wbits % 9))
         growth = 1
     if batch_k_max is None:
@@ -287,6 +317,8 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
         on_gpu = buf.device.type == "cuda"
         hbuf = torch.empty(3, dtype=torch.int64, pin_memory=True) if on_gpu else buf
     slot = board.begin() if board is not None else None
+    if attach_fn is None:
+        attach_fn = lambda s: None  # noqa: E731
     if slot is not None:
         attach_fn(slot)
     bound = DPOW_NO_HIT

@@ -25,9 +25,11 @@ extern "C" {
 #endif
 
 /* 2: dpow_worker_result gained `error` (dpow_worker.h), DPOW_K_LIMIT = 2^55 - 1 and
- * 7-byte chunks (round 2); dpow_node_* (round 3).  A consumer built against
- * another version must refuse the library. */
-#define DPOW_ABI_VERSION 2
+ * 7-byte chunks (round 2); dpow_node_* (round 3).
+ * 3 (round 4): dpow_diag_launch_geometry takes ntz (dpow_diag.h); dpow_node_release.
+ * A consumer built against another version must refuse the library before any
+ * other call (distpow/_lib.py check_abi, tests/c/abi_harness.c). */
+#define DPOW_ABI_VERSION 3
 
 /* "no hit" sentinel for global indices: INT64_MAX, so that signed (RCCL/gloo
  * int64 MIN) and unsigned (device atomicMin u64) reductions agree. */
@@ -122,8 +124,10 @@ int dpow_search_bound(dpow_ctx *ctx, uint64_t global_idx);
  *   - returns DPOW_CANCELLED when the slot's stop is raised, and raises it when
  *     it returns DPOW_CANCELLED or an error itself, so a cancelled or failed rank
  *     ends the node's search on every GPU at once.
- * The node's answer is still the minimum over the ranks' results (distpow.node:
- * one RCCL MIN all-reduce per batch), which equals the workerBits = 0 first hit.
+ * The node's answer is still the minimum over the ranks' results, taken once per
+ * batch (distpow.node.node_mine): through dpow_node_vote below when every rank
+ * shares the host, else one RCCL MIN all-reduce.  It equals the workerBits = 0
+ * first hit.
  * ------------------------------------------------------------------------- */
 typedef struct dpow_node_slot {
     uint64_t best;     /* lowest verified hit of any rank; DPOW_NO_HIT = none */
@@ -131,8 +135,15 @@ typedef struct dpow_node_slot {
     uint32_t pad[13];  /* one 64-byte line per slot */
 } dpow_node_slot;
 /* Attach a slot to ctx for its next searches (NULL detaches).  Not thread-safe
- * against a running search on ctx. */
+ * against a running search on ctx.  The slot's host page is registered with HIP once
+ * per process and stays registered while any context that attached it is open, so
+ * detaching and re-attaching costs nothing and several contexts may share a slot. */
 int dpow_node_attach(dpow_ctx *ctx, dpow_node_slot *slot);
+/* Memory holding slots is about to be unmapped: waits for the launches of every
+ * context that attached a slot in [mem, mem + len), then drops the library's HIP
+ * registration of those pages (so a later mapping at the same address is registered
+ * afresh).  DPOW_EINVAL if a context is still attached to a slot there (ABI 3). */
+int dpow_node_release(void *mem, size_t len);
 /* best = DPOW_NO_HIT, stop = 0 (before the node's search that uses the slot). */
 void dpow_node_slot_reset(dpow_node_slot *slot);
 /* Atomic min of a verified hit into the slot. */

@@ -50,11 +50,15 @@ int dpow_diag_launch_latency(int device, int mode, int reps, double *median_us);
 int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint64_t k,
                          uint32_t iv_d, uint32_t state_d);
 
-/* Claim geometry dpow_search gives each launch of a window (host logic, no GPU):
- * the planner's launches sized for a grid of at most max_blocks worker workgroups
- * (dpow_search passes CUs x 6 / searches in flight on the device).  One entry per
- * launch; returns the number of launches (only the first max_launches are written),
- * or < 0 when a launch would leave a claim counter without waves. */
+/* Claim geometry dpow_search gives each launch of a window (host logic, no GPU), sized by
+ * the same function dpow_search uses (plan.cpp size_search_launch): the device share
+ * (cus x the ntz- and size-dependent workgroups per CU / share, at least one per claim
+ * counter), the expected first hit at ntz, the minimum chunk, the claims per wave and the
+ * poll group.  `share` is the number of searches in flight on the device (1 alone).  One
+ * entry per launch; returns the number of launches (only the first max_launches are
+ * written), or < 0 when a launch would leave a claim counter without waves.
+ * (ABI 3: ntz, cus and share replace round 3's max_blocks, which sized every launch as an
+ * ntz-less full grid and so never covered the short searches' grids.) */
 typedef struct dpow_diag_launch {
     uint64_t k_begin, k_end;      /* chunk range */
     uint64_t i_begin, i_end;      /* local index range */
@@ -66,10 +70,12 @@ typedef struct dpow_diag_launch {
     uint32_t rbits;               /* R = 2^rbits thread bytes per k */
     uint32_t wave_block;          /* local indices per wave-block */
     uint64_t n_static;            /* claims handed out by wave index (the "_ls" kernels' static first claims) */
+    uint32_t poll_wb;             /* wave-blocks per poll group */
+    uint32_t pad;
 } dpow_diag_launch;
-int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t worker_byte,
-                              uint32_t worker_bits, uint64_t k_begin, uint64_t k_end,
-                              uint64_t max_blocks, dpow_diag_launch *out, size_t max_launches);
+int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,
+                              uint32_t worker_bits, uint64_t k_begin, uint64_t k_end, uint32_t cus,
+                              uint32_t share, dpow_diag_launch *out, size_t max_launches);
 
 /* Worker workgroups per CU dpow_search gives a launch of `candidates` local indices
  * at (ntz, worker_bits), before dividing by the searches sharing the device: 6 (the

@@ -42,6 +42,13 @@ static int traced(dpow_worker *w, const char *action) {
 }
 
 int main(int argc, char **argv) {
+    /* A consumer built against another ABI version refuses the library (dpow.h) before it
+     * calls anything else: struct layouts and signatures may differ. */
+    if (dpow_abi_version() != DPOW_ABI_VERSION) {
+        fprintf(stderr, "abi_harness: libdpow.so implements ABI %d, this program was built for %d: refused\n",
+                dpow_abi_version(), DPOW_ABI_VERSION);
+        return 3;
+    }
     const uint8_t nonce[4] = {1, 2, 3, 4};
     uint8_t secret[DPOW_MAX_SECRET];
     size_t len = 0;
@@ -61,7 +68,6 @@ int main(int argc, char **argv) {
     if (n != 3 || !plan[0].start_kernel || plan[1].chunk_len != 1 || plan[1].chunk_len_last != 3 ||
         plan[2].chunk_len != 4)
         return fail("dpow_plan_window");
-    if (dpow_abi_version() != DPOW_ABI_VERSION) return fail("dpow_abi_version");
     /* the node slot (host memory shared by a node's ranks): reset, post = atomic min, stop */
     dpow_node_slot slot;
     dpow_node_slot_reset(&slot);

@@ -4,6 +4,7 @@ import glob
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -47,8 +48,65 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_device_count():
     import distpow
-    assert distpow.lib().dpow_abi_version() == 2
+    from distpow import _lib
+    assert distpow.lib().dpow_abi_version() == _lib.header_abi_version() == 3
     assert distpow.device_count() >= 0
+
+
+def _stub_library(tmp_path, abi, omit=()):
+    """A libdpow.so stand-in: every function the headers declare, each aborting when
+    called, except dpow_abi_version, which reports `abi`."""
+    src = ["#include <stdlib.h>", f"int dpow_abi_version(void) {{ return {abi}; }}"]
+    src += [f"void {n}(void) {{ abort(); }}" for n in sorted(declared_functions())
+            if n != "dpow_abi_version" and n not in omit]
+    d = tmp_path / f"stub_abi{abi}"
+    d.mkdir()
+    (d / "stub.c").write_text("\n".join(src) + "\n")
+    so = d / "libdpow.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(d / "stub.c")])
+    return str(so)
+
+
+def _load_in_child(so):
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import distpow\n"
+            "try:\n"
+            "    distpow.lib()\n"
+            "except ImportError as e:\n"
+            "    print('REFUSED', e); sys.exit(7)\n"
+            "print('LOADED')\n") % os.path.join(ROOT, "distributed-proof-of-work_amd")
+    env = dict(os.environ, DPOW_LIB_PATH=so)
+    return subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+
+
+def test_library_of_another_abi_is_refused(tmp_path):
+    """the binding compares dpow_abi_version() with include/dpow.h's
+    DPOW_ABI_VERSION for every library, DPOW_LIB_PATH overrides included, and raises
+    ImportError without calling anything else (the stub aborts on any other call)."""
+    r = _load_in_child(_stub_library(tmp_path, 1))
+    assert r.returncode == 7, (r.stdout, r.stderr)
+    assert "REFUSED" in r.stdout and "DPOW_ABI_VERSION 1" in r.stdout
+
+
+def test_library_missing_entry_points_is_refused(tmp_path):
+    """The right version number but a missing entry point: refused too (no silent skip)."""
+    r = _load_in_child(_stub_library(tmp_path, 3, omit=("dpow_search_bound",)))
+    assert r.returncode == 7, (r.stdout, r.stderr)
+    assert "dpow_search_bound" in r.stdout
+
+
+def test_c_harness_refuses_another_abi(tmp_path):
+    """tests/c/abi_harness.c (the cgo stand-in) makes the same check first: exit 3 on an
+    ABI-1 library, before any other call (which would abort)."""
+    so = _stub_library(tmp_path, 1)
+    libdir = os.path.dirname(so)
+    exe = str(tmp_path / "abi_harness_stub")
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "abi_harness.c"), "-L", libdir, "-ldpow",
+                           f"-Wl,-rpath,{libdir}", "-pthread", "-o", exe])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "refused" in r.stderr
 
 
 def test_open_without_gpu_fails_loudly():
@@ -100,7 +158,7 @@ def test_c_abi_from_plain_c(tmp_path):
     distpow.lib()  # the build-id check
     out = subprocess.check_output([_build_c_harness(tmp_path)], timeout=60).decode()
     rec = json.loads(out)
-    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 2
+    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 3
 
 
 @pytest.mark.gpu

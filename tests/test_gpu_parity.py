@@ -607,6 +607,59 @@ def test_node_stop_ends_a_running_search(miner):
     assert r.status == FOUND
 
 
+def _stopped_by_node(miner, lib, addr):
+    """A running unreachable search on `miner` ends CANCELLED when the slot's stop is raised."""
+    lib.dpow_node_slot_reset(addr)
+    out = {}
+    th = threading.Thread(target=lambda: out.update(r=miner.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, 1 << 40),
+                                                   t=time.perf_counter()))
+    th.start()
+    time.sleep(0.2)
+    t0 = time.perf_counter()
+    lib.dpow_node_stop(addr)
+    th.join(timeout=30)
+    assert not th.is_alive() and out["r"].status == CANCELLED
+    return out["t"] - t0
+
+
+def test_two_contexts_share_a_slot_one_closes(miner, golden):
+    """the slot's host page is registered once per process and held by
+    every context that attached it (dpow_api.cpp page registry).  Two contexts attach one
+    slot; closing one must not unregister the page under the other, whose kernels' watcher
+    still stops at the node's stop and bound.  dpow_node_release refuses while a context is
+    attached and, once detached, drops the registration; attaching again registers afresh."""
+    slot = _Slot()
+    addr = ctypes.addressof(slot)
+    lib = distpow.lib()
+    lib.dpow_node_slot_reset(addr)
+    other = distpow.Miner(0)
+    try:
+        other.attach_node(addr)
+        miner.attach_node(addr)
+        assert other.search([1, 2, 3, 4], 3, 0, 0, 0, 1 << 10).status == FOUND  # other's launches used the page
+    finally:
+        other.close()  # drops other's hold; the miner's keeps the page registered
+    try:
+        assert _stopped_by_node(miner, lib, addr) < 0.25
+        # the node's best through the page: a bound below the answer leaves nothing to find
+        e = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 7)
+        lib.dpow_node_slot_reset(addr)
+        lib.dpow_node_post(addr, e["global_idx"] - 1)
+        assert miner.search([1, 2, 3, 4], 7, 0, 0, 0, 1 << 26).status == EXHAUSTED
+        lib.dpow_node_slot_reset(addr)
+        assert lib.dpow_node_release(addr, ctypes.sizeof(slot)) == -1  # still attached
+    finally:
+        miner.attach_node(None)
+    assert lib.dpow_node_release(addr, ctypes.sizeof(slot)) == 0
+    miner.attach_node(addr)  # registered afresh
+    try:
+        assert _stopped_by_node(miner, lib, addr) < 0.25
+    finally:
+        miner.attach_node(None)
+    r = miner.search([1, 2, 3, 4], 7, 0, 0, 0, 1 << 26)
+    assert r.status == FOUND and r.global_idx == e["global_idx"]
+
+
 def test_concurrent_searches_share_the_gpu(golden):
     """Four contexts searching at once on one GPU (each sizes its grids to its share of the
     device, dpow_api.cpp ActiveSearch): every answer is still the golden, and a concurrent

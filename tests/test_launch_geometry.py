@@ -28,20 +28,30 @@ class DiagLaunch(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("k_begin", "k_end", "i_begin", "i_end", "wb_begin", "n_wblocks",
                                                 "n_big", "n_chunks", "worker_blocks")] + \
                [(n, ctypes.c_uint32) for n in ("chunk", "chunk_tail", "rbits", "wave_block")] + \
-               [("n_static", ctypes.c_uint64)]
+               [("n_static", ctypes.c_uint64), ("poll_wb", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
-def geometry(nonce, wb, wbits, k0, k1, max_blocks):
+def geometry(nonce, wb, wbits, k0, k1, cus, share=1, ntz=32):
+    """The launches dpow_search(nonce, ntz, wb, wbits, k0, k1) queues on a device of `cus`
+    CUs shared by `share` searches, sized by the search's own function (size_search_launch)."""
     L = distpow.lib()
     fn = L.dpow_diag_launch_geometry
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
-                   ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(DiagLaunch), ctypes.c_size_t]
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                   ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(DiagLaunch),
+                   ctypes.c_size_t]
     n = bytes(nonce)
     arr = (DiagLaunch * 16)()
-    cnt = fn(n, len(n), wb, wbits, k0, k1, max_blocks, arr, 16)
+    cnt = fn(n, len(n), ntz, wb, wbits, k0, k1, cus, share, arr, 16)
     assert cnt >= 0, distpow._lib.last_error()
+    assert cnt <= 16
     return list(arr[:cnt])
+
+
+def grid_cap(cus, share=1):
+    """The most worker workgroups a launch can get: the full 6-per-CU grid's share, at least
+    one per claim counter."""
+    return max(cus * 6 // share, CLAIM_COUNTERS)
 
 
 def check(d, max_blocks):
@@ -89,9 +99,10 @@ def check(d, max_blocks):
             assert lo // seg_i == hi // seg_i, (d.k_begin, d.k_end, s, sz)
 
 
-@pytest.mark.parametrize("max_blocks", [8, 192, 1536])
-def test_boundary_straddling_windows(max_blocks):
-    rnd = random.Random(max_blocks)
+@pytest.mark.parametrize("cus", [1, 32, 256])
+def test_boundary_straddling_windows(cus):
+    max_blocks = grid_cap(cus)
+    rnd = random.Random(cus)
     for _ in range(400):
         wbits = rnd.choice([0, 1, 2, 3, 5, 8, 9, 10])
         wb = rnd.randrange(1 << (wbits % 9)) if wbits % 9 else 0
@@ -105,7 +116,7 @@ def test_boundary_straddling_windows(max_blocks):
         k0 = max(1 << 24, edge - rnd.randrange(1, 3000))
         k1 = min(distpow.DPOW_K_LIMIT, edge + rnd.randrange(1, 3000))
         nonce = [rnd.randrange(256) for _ in range(rnd.choice([0, 3, 4, 7, 55, 60, 64]))]
-        for d in geometry(nonce, wb, wbits, k0, k1, max_blocks):
+        for d in geometry(nonce, wb, wbits, k0, k1, cus, ntz=rnd.choice([32, 7, 8, 9])):
             check(d, max_blocks)
 
 
@@ -117,36 +128,73 @@ def test_large_and_small_windows():
         k0 = rnd.choice([0, 1, 255, 70000, (1 << 24) - 1, 1 << 24, rnd.randrange(1 << 32), (1 << 32) + 5,
                          rnd.randrange(1 << 40, 1 << 48), rnd.randrange(1 << 48, distpow.DPOW_K_LIMIT)])
         k1 = min(distpow.DPOW_K_LIMIT, k0 + rnd.choice([1, 2, 7, 64, 5000, 1 << 20, 1 << 26, 1 << 31]))
-        for max_blocks in (8, 96, 768, 1024, 1536):  # shares and the 3 / 4 / 6-per-CU grids
+        ntz = rnd.choice([32, 3, 5, 6, 7, 8, 9])
+        for cus, share in ((1, 1), (16, 1), (256, 8), (256, 2), (256, 1)):  # shares, the 2 / 3 / 4 / 6-per-CU grids
             for nonce in ([1, 2, 3, 4], [1, 2]):  # SH 0; SH 2 (word W0+2 splits at L = 6)
-                for d in geometry(nonce, wb, wbits, k0, k1, max_blocks):
-                    check(d, max_blocks)
+                for d in geometry(nonce, wb, wbits, k0, k1, cus, share, ntz):
+                    check(d, grid_cap(cus, share))
 
 
-def test_chunk_length_spanning_launches():
-    """Windows across k = 1, 256 and 65536 for SH = 0 nonces: one md5 launch spans the chunk
-    lengths (after the start kernel's k = 0), and its claims respect the boundaries."""
-    rnd = random.Random(7)
-    for _ in range(300):
+def lspan_end(ntz, rbits):
+    """plan.cpp lspan_end: chunk lengths 1..3 share a launch (up to k = 2^24) when the first
+    hit is expected within 2^28 candidates of the partition, else only lengths 1..2."""
+    expect = ((16 ** ntz) << rbits) >> 8 if ntz < 14 else None
+    return 1 << 24 if expect is not None and expect <= 1 << 28 else 1 << 16
+
+
+@pytest.mark.parametrize("ntz", [3, 4, 5, 6, 7, 8, 9, 32])
+def test_chunk_length_spanning_launches(ntz):
+    """Windows across k = 1, 256 and 65536 for SH = 0 nonces, at every N a short search runs
+    with (the grids, chunks and static first claims of short searches): one md5
+    launch spans the chunk lengths (after the start kernel's k = 0) up to lspan_end, and its
+    claims respect the boundaries."""
+    rnd = random.Random(7 + ntz)
+    for _ in range(150):
         wbits = rnd.choice([0, 1, 2, 3, 5, 7])
         wb = rnd.randrange(1 << wbits) if wbits else 0
         k0 = rnd.choice([0, 1, 2, 200, 255, 256, 300, 65000, 65535])
         k1 = min(1 << 24, k0 + rnd.choice([2, 60, 300, 5000, 70000, 1 << 20, 1 << 24]))
         nonce = [rnd.randrange(256) for _ in range(rnd.choice([0, 4, 8, 44, 48, 60, 64]))]
-        ds = geometry(nonce, wb, wbits, k0, k1, rnd.choice([8, 768, 1536]))
-        assert len(ds) == 1, (len(nonce), k0, k1, [(d.k_begin, d.k_end) for d in ds])
-        assert ds[0].k_begin == max(k0, 1) and ds[0].k_end == k1
+        cus, share = rnd.choice([(1, 1), (128, 1), (256, 1), (256, 8)])
+        ds = geometry(nonce, wb, wbits, k0, k1, cus, share, ntz)
+        le = lspan_end(ntz, 8 - wbits)
+        assert ds[0].k_begin == max(k0, 1) and ds[-1].k_end == k1
+        assert all(a.k_end == b.k_begin for a, b in zip(ds, ds[1:]))
+        if k1 <= le or max(k0, 1) >= le:
+            assert len(ds) == 1, (len(nonce), k0, k1, [(d.k_begin, d.k_end) for d in ds])
+        else:
+            assert len(ds) == 2 and ds[0].k_end == le
         for d in ds:
-            check(d, 1536)
+            check(d, grid_cap(cus, share))
+            assert d.poll_wb in (1, 4, 16)
 
 
 def test_bench_step_is_one_launch():
     """The bench step (2^28 k from 2^24 at workerBits 0) and an 8-GPU rank's step (2^31 k at
     workerBits 3) are one launch each: launches span the 2^24-k segments."""
     for wb, wbits, nk in ((0, 0, 1 << 28), (5, 3, 1 << 31)):
-        ds = geometry([1, 2, 3, 4], wb, wbits, 1 << 24, (1 << 24) + nk, 1536)
-        assert len(ds) == 1 and ds[0].chunk == 32 and ds[0].worker_blocks == 1536
+        ds = geometry([1, 2, 3, 4], wb, wbits, 1 << 24, (1 << 24) + nk, 256)
+        assert len(ds) == 1 and ds[0].chunk == 32 and ds[0].worker_blocks == 1536 and ds[0].poll_wb == 16
         check(ds[0], 1536)
+
+
+def test_short_search_grids():
+    """The grids dpow_search gives short searches (the geometry diagnostic runs the search's
+    own sizing): an 8-GPU rank's N = 6 window gets 2 workgroups per CU, claims of 2
+    wave-blocks, a poll after every wave-block and static first claims; one GPU's N = 7 the
+    full grid with 4-wave-block poll groups, its N = 6 4 workgroups per CU."""
+    # [1,2,3,4]/6 on a workerBits-3 rank (R = 32): 16^6 * 32 / 256 = 2^21 expected candidates
+    d, = geometry([1, 2, 3, 4], 5, 3, 1, 1 << 24, 256, ntz=6)
+    assert d.worker_blocks <= 2 * 256 and d.chunk_tail <= 2 and d.poll_wb == 1 and d.n_static > 0
+    check(d, grid_cap(256))
+    # [1,2,3,4]/7 at one GPU: 2^28 expected candidates, past kMidExpect (2^26): the full 6 per
+    # CU; below kFastPollCands (2^30): poll groups of 4
+    d, = geometry([1, 2, 3, 4], 0, 0, 1, 1 << 20, 256, ntz=7)
+    assert d.worker_blocks == 1536 and d.poll_wb == 4
+    check(d, grid_cap(256))
+    d, = geometry([1, 2, 3, 4], 0, 0, 1, 1 << 20, 256, ntz=6)  # 2^24 expected: 4 per CU
+    assert d.worker_blocks == 1024 and d.poll_wb == 4
+    check(d, grid_cap(256))
 
 
 def test_grid_policy_for_short_launches():

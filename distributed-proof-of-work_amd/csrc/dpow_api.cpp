@@ -86,11 +86,17 @@ constexpr size_t kRing = 8;  // completion records and event pairs, indexed by l
 // 64-bit bound injected by dpow_search_bound (Launch::ext_bound, relayed by the watcher).
 constexpr size_t kStaleWord = 8;
 constexpr size_t kBoundWord = 16;  // uint32 index of an 8-byte-aligned 64-bit word
+constexpr size_t kEarlyWord = 20;  // uint32 index of kCtrlRing 64-bit early-hit words (Launch::early)
 constexpr size_t kCancelPage = 128;
-// Completion-record wait: spin for the first kSpinNs of a search (time-to-secret),
-// then poll at kPollNs (20 us in round 2: a record waited up to that long to be seen once
-// a search ran past the spin; the thread sleeps between polls either way).
+static_assert(kEarlyWord * 4 + kCtrlRing * 8 <= kCancelPage, "the early-hit words fit the pinned page");
+// Completion-record wait: spin for the first kSpinNs of a search (time-to-secret) -- or
+// longer, up to kSpinMaxNs, for twice the time its first hit is expected in (round 3 spun for
+// 200 us only, so an 8-GPU rank's N = 7 search, whose hit comes ~200 us in, saw its records
+// and posted its hit one 5-7 us sleep late) -- then poll at kPollNs (20 us in round 2: a
+// record waited up to that long to be seen once a search ran past the spin; the thread
+// sleeps between polls either way).
 constexpr int64_t kSpinNs = 200000;
+constexpr int64_t kSpinMaxNs = 4000000;
 constexpr long kPollNs = 5000;
 constexpr int64_t kNoDeadline = INT64_MAX;
 // Deferred queueing.  A launch is queued only once the launches ahead of it are
@@ -141,9 +147,17 @@ int64_t now_ns() {
 // (dpow_node_attach) as last seen.
 struct SearchWait {
     int64_t t0 = now_ns();
+    int64_t spin_ns = kSpinNs;  // spin_for(): this search's spin window
     long old_slack = -1;
     uint64_t node_seen = DPOW_NO_HIT;  // lowest node best injected into this search
     bool node_stop = false;            // the node slot's stop was seen
+    // Early Found fan-out (attached node): the pinned word the running launch's watcher relays
+    // Ctrl::best to, the lowest value seen there, and what a hit is verified against.
+    const uint64_t *early = nullptr;
+    uint64_t early_seen = DPOW_NO_HIT;
+    const uint8_t *nonce = nullptr;
+    size_t nonce_len = 0;
+    uint32_t ntz = 0;
     void lower_slack() {
         if (old_slack >= 0) return;
         // Linux pads a normal thread's nanosleep by its 50 us default timer slack,
@@ -236,6 +250,22 @@ int poll_node(dpow_ctx *c, SearchWait &sw) {
     return 0;
 }
 
+// The early-hit word (attached node): a value below what was seen there is this launch's
+// Ctrl::best -- a hit of ours, or a bound that is itself a hit of another rank.  It is
+// verified with the host MD5 and posted to the node slot at once, so the other ranks stop at
+// it while this launch drains; the search's final answer is still taken from the records.
+void poll_early(dpow_ctx *c, SearchWait &sw) {
+    const uint64_t g = __atomic_load_n(sw.early, __ATOMIC_ACQUIRE);
+    if (g >= sw.early_seen) return;
+    sw.early_seen = g;
+    uint8_t sec[DPOW_MAX_SECRET];
+    size_t len = 0;
+    if (dpow_secret_from_index(g, sec, &len) != 0) return;
+    if (!dpow_verify(sw.nonce, sw.nonce_len, sec, len, sw.ntz)) return;  // never expected: left to the record
+    dpow_node_post(c->node, g);
+    if (c->diag_t[7] < 0) c->diag_t[7] = now_ns() - sw.t0;
+}
+
 // Wait for the completion record of launch `seq`, until `deadline` (now_ns()
 // clock; kNoDeadline: none).  Returns 1 when the record is there, 0 at the
 // deadline, < 0 on error.  Spins in the first kSpinNs of the search (the record
@@ -249,7 +279,7 @@ int wait_record(dpow_ctx *c, uint64_t seq, int64_t deadline, SearchWait &sw) {
         if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return 1;
         const int64_t t = now_ns();
         if (t >= deadline) return 0;
-        const bool spinning = t - sw.t0 < kSpinNs;
+        const bool spinning = t - sw.t0 < sw.spin_ns;
         if (spinning ? (it % 4096 == 0) : (it % 16 == 0)) {
             const hipError_t q = hipStreamQuery(c->slots[seq % kRing].stream);
             if (q == hipSuccess) {
@@ -258,6 +288,7 @@ int wait_record(dpow_ctx *c, uint64_t seq, int64_t deadline, SearchWait &sw) {
             }
             if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
         }
+        if (sw.early && (!spinning || it % 8 == 0)) poll_early(c, sw);
         if (c->node && (!spinning || it % 64 == 0)) {
             const int rc = poll_node(c, sw);
             if (rc < 0) return rc;
@@ -304,6 +335,10 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     if (c->device >= kMaxDevices) return set_error(DPOW_EINVAL, "dpow_search: device ordinal too large");
     const ActiveSearch active(c->device);
     SearchWait sw;
+    {   // spin while the first hit is expected (memoryless: from any start), 2x, within [kSpinNs, kSpinMaxNs]
+        const double expect_ns = (double)expected_first_hit(ntz, remainder_bits(worker_bits)) / kEstRate * 1e9;
+        sw.spin_ns = (int64_t)std::min<double>(std::max<double>(2.0 * expect_ns, (double)kSpinNs), (double)kSpinMaxNs);
+    }
 
     {   // keep the stale mark within 2^30 launches of the present (int32 distance in the watcher)
         uint32_t *st = &c->h_cancel[kStaleWord];
@@ -318,6 +353,14 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     sw.node_seen = node_best;
     const uint64_t seq0 = c->seq;
     for (int64_t &t : c->diag_t) t = -1;
+    if (c->node) {  // the early Found fan-out: this search's control block's early-hit word
+        uint64_t *ew = reinterpret_cast<uint64_t *>(c->h_cancel + kEarlyWord) + c->ctrl_idx;
+        __atomic_store_n(ew, (uint64_t)DPOW_NO_HIT, __ATOMIC_RELEASE);
+        sw.early = ew;
+        sw.nonce = nonce;
+        sw.nonce_len = nonce_len;
+        sw.ntz = ntz;
+    }
     size_t launched = 0, consumed = 0;
     int64_t busy_until = 0;  // expected end of the launches queued so far (now_ns clock)
     PlannedLaunch pl;
@@ -490,6 +533,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         L.seq = (uint32_t)(seq + 1);
         L.node_best = c->d_node ? reinterpret_cast<const unsigned long long *>(&c->d_node->best) : nullptr;
         L.node_stop = c->d_node ? &c->d_node->stop : nullptr;
+        L.early = c->d_node ? reinterpret_cast<unsigned long long *>(c->d_cancel + kEarlyWord) + c->ctrl_idx : nullptr;
         e = search_launch((int)pl.info.nblk, (int)pl.info.w0, (int)pl.info.sh, L, (uint32_t)(worker_blocks + 1),
                           c->stream);
         if (e != hipSuccess) return hip_fail(e, "search_launch");

@@ -150,6 +150,12 @@ struct Launch {
     // lowers Ctrl::best, a raised stop stops the launch.
     const unsigned long long *node_best;
     const uint32_t *node_stop;
+    // Early hit word (attached node only; null otherwise): pinned, host-coherent.  The watcher
+    // relays Ctrl::best here as soon as it drops, so the host can verify and post a hit to the
+    // node slot while the launch still drains (the Found fan-out no longer waits for the
+    // launch's completion record).  One word per control block of the ring (a stale launch of
+    // the previous search writes its own block's word).
+    unsigned long long *early;
     // SH = 0 layouts below k = 2^24: T / KT hold the message of chunk length 0 (the pad at
     // byte 1 of word W0, bit length 8 (nonce_len + 1)) with the launch's block count, and a
     // candidate of chunk length l adds lseg_deltas(l) to words W0, W0 + 1 and the bit-length

@@ -109,19 +109,38 @@ namespace DPOW_KNS {
 #ifndef DPOW_STATIC_FIRST
 #define DPOW_STATIC_FIRST DPOW_VLS
 #endif
+// The claim-ahead atomic in the chunk's last poll group instead of its first (one-block
+// kernels): a wave then reserves its next chunk only near the end of the current one, so a
+// slow wave does not sit on an early chunk for the whole of its current one, and the polls of
+// the chunk's earlier groups do not wait for the claim atomic (vmcnt counts in issue order).
+#ifndef DPOW_CLAIM_LATE
+#define DPOW_CLAIM_LATE 0
+#endif
+// A fresh read of Ctrl::best / Ctrl::stop at the end of each chunk (one-block kernels), for
+// the check at the next claim: the group's poll was issued at the group's start, so a wave
+// whose chunk ended after a hit elsewhere would start one more chunk above it and hash a
+// whole group of it (tools/wave_trace_node.py: the last waves of an 8-GPU rank's
+// [1,2,3,4]/7 search exited 8-28 us after the hit, on chunks above it).  Issued before the
+// claim is taken, consumed at the check: its latency overlaps the claim's.
+#ifndef DPOW_CLAIM_FRESH
+#define DPOW_CLAIM_FRESH 0
+#endif
 #ifndef DPOW_CLAIM_DEFER
 #define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch;
                             // one final block only, search_body kDeferClaims)
 #endif
-// Diagnostic builds only (tools/wave_trace.py): every worker wave records
-// {start, first claim, exit} in s_memrealtime ticks (100 MHz) and its hashed
-// wave-blocks, read back with dpow_diag_wave_trace.
+// Diagnostic builds only (tools/wave_trace.py, tools/wave_trace_node.py): every worker wave
+// records kTraceFields words -- {start, first claim, exit} in s_memrealtime ticks (100 MHz),
+// its hashed wave-blocks, the start of its last chunk and that chunk's claim index, why it
+// left the claim loop (1 counters drained, 2 a chunk at or above the best, 3 stop) and when
+// it found a hit of its own (0: none) -- read back with dpow_diag_wave_trace.
 #ifndef DPOW_WAVE_TRACE
 #define DPOW_WAVE_TRACE 0
 #endif
 #if DPOW_WAVE_TRACE
 constexpr uint32_t kTraceWaves = 8192;
-static __device__ unsigned long long g_wave_trace[kTraceWaves * 4];
+constexpr uint32_t kTraceFields = 8;
+static __device__ unsigned long long g_wave_trace[kTraceWaves * kTraceFields];
 #endif
 
 template <int I>
@@ -720,6 +739,12 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 //
 // The bound injected by dpow_search_bound (a pinned host word) is relayed the same way.
 //
+// With a node slot attached it also relays Ctrl::best the other way, to the pinned early-hit
+// word (Launch::early): a hit of this launch reaches the host ~1 us after the wave's
+// atomicMin, which verifies it and posts it to the node slot at once -- the other ranks stop
+// at it while this launch is still draining the chunks below it (round 3: the post waited
+// for the completion record, the drain plus ~5 us).
+//
 // It also stamps the launch's start (s_memrealtime into the claim slot's spare word): the
 // watcher workgroup is dispatched first, and the kernel time in the completion record
 // replaces per-launch HIP timing events, whose profiling packets cost the host ~4.5 us per
@@ -727,10 +752,32 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 DPOW_DEV void watcher(const Launch &L) {
     if (threadIdx.x != 0) return;
     __hip_atomic_store(&L.claim[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long node_seen = ~0ull, bound_seen = L.bound0;
+    unsigned long long node_seen = ~0ull, bound_seen = L.bound0, early_seen = kNoHit;
+#if DPOW_WAVE_TRACE
+    // the watcher's own record, in the last trace slot: start, the first node best relayed,
+    // the first early-hit relay, exit
+    unsigned long long *wt = g_wave_trace + kTraceFields * (kTraceWaves - 1);
+    wt[0] = __builtin_amdgcn_s_memrealtime();
+    wt[1] = wt[2] = 0;
+#endif
     for (;;) {
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done >= L.done_target) return;
+        if (done >= L.done_target) {
+#if DPOW_WAVE_TRACE
+            wt[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+            return;
+        }
+        if (L.early) {
+            const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b < early_seen) {
+#if DPOW_WAVE_TRACE
+                if (wt[2] == 0) wt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+                early_seen = b;
+                __hip_atomic_store(L.early, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
         const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         bool stop = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
                     (int32_t)(stale - L.seq) >= 0;
@@ -742,6 +789,9 @@ DPOW_DEV void watcher(const Launch &L) {
         if (L.node_best) {
             const unsigned long long nb = __hip_atomic_load(L.node_best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (nb < node_seen) {
+#if DPOW_WAVE_TRACE
+                if (wt[1] == 0 && nb < kNoHit) wt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
                 node_seen = nb;
                 __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -898,7 +948,7 @@ DPOW_DEV void search_body(const Launch &L) {
     }
 #if DPOW_WAVE_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    unsigned long long t_first = 0, n_wb = 0;
+    unsigned long long t_first = 0, n_wb = 0, t_last = 0, c_last = 0, reason = 0, t_hit = 0;
 #endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t loff = lane_offset(L.rbits, lane);
@@ -946,6 +996,8 @@ DPOW_DEV void search_body(const Launch &L) {
     // or shifts their register assignment (-5 to -10 %, profiles/r02_ab_layouts/), so
     // they keep the claim read in front of the chunk.
     constexpr bool kDeferClaims = DPOW_CLAIM_DEFER && NBLK == 1;
+    constexpr bool kLate = DPOW_CLAIM_LATE && kDeferClaims && DPOW_POLL_WB > 0;
+    constexpr bool kFresh = DPOW_CLAIM_FRESH && NBLK == 1;
     uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
 #if DPOW_STATIC_FIRST
@@ -967,6 +1019,9 @@ DPOW_DEV void search_body(const Launch &L) {
         // on a slower XCD).  A counter only ever drains, so after a full round
         // of drained counters every chunk has been handed out.
         if (claim >= L.n_chunks) {
+#if DPOW_WAVE_TRACE
+            reason = 1;
+#endif
             if (skip || ++hops >= kClaimCounters) break;
             x = (x + 1u) % kClaimCounters;
             const unsigned long long seen =
@@ -984,7 +1039,9 @@ DPOW_DEV void search_body(const Launch &L) {
         // this chunk (claim_take): the wave hashes while the atomic is in flight.
         unsigned long long next_v = 0;
         uint64_t next = 0;
-        if constexpr (kDeferClaims) next_v = claim_issue<true>(L.claim + x * kClaimStride, lane);
+        bool issued = false;  // kLate: the next claim's atomic was issued (in the chunk's last group)
+        if constexpr (kLate) (void)issued;
+        else if constexpr (kDeferClaims) next_v = claim_issue<true>(L.claim + x * kClaimStride, lane);
         else next = claim_next(L.claim + x * kClaimStride, x, lane, cbase);
 #endif
         // Claims [0, n_big) are `chunk` wave-blocks, the rest `chunk_tail`: the
@@ -1010,8 +1067,16 @@ DPOW_DEV void search_body(const Launch &L) {
         // or above the best index found so far.
         // Everything below the best has been or is being hashed by earlier claims.
         if (stop != 0u ||
-            global_of_local(i_first < L.i_begin ? L.i_begin : i_first, L.rbits, L.base_tb) >= best)
+            global_of_local(i_first < L.i_begin ? L.i_begin : i_first, L.rbits, L.base_tb) >= best) {
+#if DPOW_WAVE_TRACE
+            reason = stop != 0u ? 3 : 2;
+#endif
             break;
+        }
+#if DPOW_WAVE_TRACE
+        t_last = __builtin_amdgcn_s_memrealtime();
+        c_last = claim;
+#endif
 #if DPOW_POLL_WB > 0
         // The chunk runs in groups of L.poll_wb wave-blocks.  Each group's loads of
         // Ctrl::best / Ctrl::stop are issued before it and consumed after it (the
@@ -1045,6 +1110,14 @@ DPOW_DEV void search_body(const Launch &L) {
             }
 #endif
             left -= q;
+#if DPOW_CLAIM_AHEAD
+            if constexpr (kLate) {
+                if (left == 0) {  // the chunk's last group: reserve the next chunk now
+                    next_v = claim_issue<true>(L.claim + x * kClaimStride, lane);
+                    issued = true;
+                }
+            }
+#endif
             const unsigned long long best_seen =
                 __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t stop_seen = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1057,6 +1130,9 @@ DPOW_DEV void search_body(const Launch &L) {
                 if (g != kNoHitG) {
                     best = g < best ? g : best;
                     hit = true;
+#if DPOW_WAVE_TRACE
+                    if (t_hit == 0) t_hit = __builtin_amdgcn_s_memrealtime();
+#endif
                     break;
                 }
             }
@@ -1081,9 +1157,28 @@ DPOW_DEV void search_body(const Launch &L) {
         best = best_next < best ? best_next : best;
         stop = stop_next;
 #endif
+        if constexpr (kFresh) {
+            const unsigned long long bf = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t sf = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            best = bf < best ? bf : best;
+            stop |= sf;
+        }
 #if DPOW_CLAIM_AHEAD
-        if constexpr (kDeferClaims) claim = claim_take(next_v, x, cbase);
-        else claim = next;
+        if constexpr (kLate) {
+            // left the chunk before its last group (a hit, a bound, a stop): every later chunk
+            // is at or above the best, or the launch is stopping -- nothing more to claim
+            if (!issued) {
+#if DPOW_WAVE_TRACE
+                reason = 4;
+#endif
+                break;
+            }
+            claim = claim_take(next_v, x, cbase);
+        } else if constexpr (kDeferClaims) {
+            claim = claim_take(next_v, x, cbase);
+        } else {
+            claim = next;
+        }
 #else
         if (stop != 0u) break;
         claim = claim_next(L.claim + x * kClaimStride, x, lane, cbase);
@@ -1099,10 +1194,15 @@ DPOW_DEV void search_body(const Launch &L) {
 #if DPOW_WAVE_TRACE
     const uint32_t wave = (blockIdx.x - 1u) * (kBlockThreads / 64) + threadIdx.x / 64u;
     if (lane == 0 && wave < kTraceWaves) {
-        g_wave_trace[4 * wave + 0] = t_start;
-        g_wave_trace[4 * wave + 1] = t_first;
-        g_wave_trace[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
-        g_wave_trace[4 * wave + 3] = n_wb;
+        unsigned long long *w = g_wave_trace + kTraceFields * wave;
+        w[0] = t_start;
+        w[1] = t_first;
+        w[2] = __builtin_amdgcn_s_memrealtime();
+        w[3] = n_wb;
+        w[4] = t_last;
+        w[5] = c_last;
+        w[6] = reason;
+        w[7] = t_hit;
     }
 #endif
     if constexpr (kDeferClaims) {

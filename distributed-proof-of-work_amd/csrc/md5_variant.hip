@@ -99,7 +99,8 @@ extern "C" int dpow_diag_wave_trace_ls(unsigned long long *out, size_t n) {
 #else
 extern "C" int dpow_diag_wave_trace(unsigned long long *out, size_t n) {
 #endif
-    if (n > dpow::DPOW_KNS::kTraceWaves * 4) n = dpow::DPOW_KNS::kTraceWaves * 4;
+    if (n > dpow::DPOW_KNS::kTraceWaves * dpow::DPOW_KNS::kTraceFields)
+        n = dpow::DPOW_KNS::kTraceWaves * dpow::DPOW_KNS::kTraceFields;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(dpow::DPOW_KNS::g_wave_trace), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
                ? 0
                : -2;

@@ -343,6 +343,7 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits)
     if (eff <= kTinyExpect) return kMaxBlocksPerCu < 2 ? kMaxBlocksPerCu : 2;
     if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
     if (eff <= kMidExpect) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
+    if (kFiveExpect && expect <= kFiveExpect) return kMaxBlocksPerCu < 5 ? kMaxBlocksPerCu : 5;
 #else
     (void)candidates, (void)ntz, (void)rbits;
 #endif

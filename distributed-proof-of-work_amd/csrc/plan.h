@@ -126,6 +126,16 @@ constexpr uint64_t kTinyExpect = 1ull << 21;
 // 52 us (tools/small_search_probe.py --stop, profiles/r03_stop_probe.json), while the owner's
 // own search is no slower (0.225 -> 0.212 ms).
 constexpr uint64_t kMidExpect = 1ull << 26;
+// Up to kFiveExpect (N = 8 on a rank of an 8-GPU node, N = 7 on one GPU): 5 workgroups per CU.
+// The SIMD's arbiter issues the oldest wave first, and with 6 waves per SIMD the youngest
+// barely progress: the chunks they claimed at the start hold up a first hit below them and the
+// drain behind it (tools/wave_trace_node.py: the owner of [2,2,2,2]/8 on an 8-GPU node hashed
+// 170 wave-blocks in its oldest waves and 20 in its youngest, whose first chunk took 250 us and
+// ended 70 us after the hit).  5 per CU costs the rate ~0.8 %.
+#ifndef DPOW_FIVE_EXPECT_LOG2
+#define DPOW_FIVE_EXPECT_LOG2 31  // 0: off (A/B switch)
+#endif
+constexpr uint64_t kFiveExpect = DPOW_FIVE_EXPECT_LOG2 ? 1ull << DPOW_FIVE_EXPECT_LOG2 : 0;
 constexpr uint64_t kTinyChunk = 2;
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits);
 // Claims per wave (chunk sizing) of a search expected to end within kFastPollCands

@@ -181,16 +181,16 @@ def test_bench_step_is_one_launch():
 def test_short_search_grids():
     """The grids dpow_search gives short searches (the geometry diagnostic runs the search's
     own sizing): an 8-GPU rank's N = 6 window gets 2 workgroups per CU, claims of 2
-    wave-blocks, a poll after every wave-block and static first claims; one GPU's N = 7 the
-    full grid with 4-wave-block poll groups, its N = 6 4 workgroups per CU."""
+    wave-blocks, a poll after every wave-block and static first claims; one GPU's N = 7 5
+    workgroups per CU with 4-wave-block poll groups, its N = 6 4 workgroups per CU."""
     # [1,2,3,4]/6 on a workerBits-3 rank (R = 32): 16^6 * 32 / 256 = 2^21 expected candidates
     d, = geometry([1, 2, 3, 4], 5, 3, 1, 1 << 24, 256, ntz=6)
     assert d.worker_blocks <= 2 * 256 and d.chunk_tail <= 2 and d.poll_wb == 1 and d.n_static > 0
     check(d, grid_cap(256))
-    # [1,2,3,4]/7 at one GPU: 2^28 expected candidates, past kMidExpect (2^26): the full 6 per
-    # CU; below kFastPollCands (2^30): poll groups of 4
+    # [1,2,3,4]/7 at one GPU: 2^28 expected candidates, past kMidExpect (2^26) and within
+    # kFiveExpect (2^31): 5 per CU; below kFastPollCands (2^30): poll groups of 4
     d, = geometry([1, 2, 3, 4], 0, 0, 1, 1 << 20, 256, ntz=7)
-    assert d.worker_blocks == 1536 and d.poll_wb == 4
+    assert d.worker_blocks == 1280 and d.poll_wb == 4
     check(d, grid_cap(256))
     d, = geometry([1, 2, 3, 4], 0, 0, 1, 1 << 20, 256, ntz=6)  # 2^24 expected: 4 per CU
     assert d.worker_blocks == 1024 and d.poll_wb == 4
@@ -200,15 +200,19 @@ def test_short_search_grids():
 def test_grid_policy_for_short_launches():
     """dpow_search's workgroups per CU (plan.cpp launch_blocks_per_cu): the full persistent
     grid for long launches with no early hit expected (the sweep), smaller grids for short
-    launches or an expected early hit (16^N R / 256 candidates of this partition)."""
+    launches or an expected early hit (16^N R / 256 candidates of this partition), 5 when the
+    hit is expected within 2^31."""
     from distpow._lib import lib
     f = lib().dpow_diag_blocks_per_cu
     assert f(1 << 36, 32, 0) == 6 and f(1 << 36, 32, 3) == 6       # the bench sweep, 1 and 8 GPUs
     assert f(1 << 22, 32, 0) == 3 and f(1 << 26, 32, 0) == 4 and f((1 << 26) + 1, 32, 0) == 6
     assert f(1 << 21, 32, 0) == 2 and f((1 << 21) + 1, 32, 0) == 3  # tiny launches (plan.h kTinyExpect)
-    assert f(1 << 32, 6, 0) == 4 and f(1 << 32, 5, 0) == 2 and f(1 << 32, 7, 0) == 6  # 16^N expected
+    assert f(1 << 32, 6, 0) == 4 and f(1 << 32, 5, 0) == 2 and f(1 << 32, 7, 0) == 5  # 16^N expected
     assert f(1 << 32, 6, 3) == 2        # 16^6 * 32 / 256 = 2^21 candidates of a workerBits-3 partition
-    assert f(1 << 32, 7, 3) == 4 and f(1 << 32, 7, 2) == 4 and f(1 << 32, 7, 1) == 6  # 2^25 / 2^26 / 2^27
+    assert f(1 << 32, 7, 3) == 4 and f(1 << 32, 7, 2) == 4 and f(1 << 32, 7, 1) == 5  # 2^25 / 2^26 / 2^27
+    # 5 per CU while a hit is expected within 2^31 candidates (plan.h kFiveExpect): an 8-GPU rank's
+    # N = 8 (2^29); one GPU's N = 8 (2^32) and an 8-GPU rank's N = 9 (2^33) keep the full grid
+    assert f(1 << 32, 8, 3) == 5 and f(1 << 32, 8, 0) == 6 and f(1 << 36, 9, 3) == 6
     assert f(1 << 32, 0, 0) == 2 and f(0, 32, 0) == 2
     for n in range(0, 40, 3):  # never more than the full grid, monotone in the launch size
         seq = [f(1 << n, z, 0) for z in range(0, 34)]

@@ -23,6 +23,7 @@ without a process group or a shared board, so its batch boundary is a no-op on t
 all-reduce (33 us at world 1) across hosts.  The ranks run one after another, each with
 the whole GPU; the 8-GPU number itself is the driver's (bench.py --gpus 8).
 """
+import ctypes
 import json
 import os
 import sys
@@ -72,11 +73,19 @@ def main():
             out["g1_ms"][f"{bytes(nonce).hex()}/{n}"] = med(ts)
 
         found_at = {}
+        tl = (ctypes.c_int64 * 8)()
 
         def search_timed(*a):
+            t_call = time.perf_counter_ns() / 1e9
             r = search(*a)
             if r.status == distpow.FOUND:
-                found_at["t"] = time.perf_counter_ns() / 1e9  # dpow_search posted its hit just before returning
+                # when the owner's hit reached the node slot: the early Found fan-out (its
+                # watcher relays the hit, the host verifies and posts it while the launch
+                # drains: dpow_diag_search_times[7], ns from dpow_search's start, which follows
+                # t_call by the ctypes call -- so this errs early by ~1-2 us), else dpow_search's
+                # own post just before it returned
+                lib.dpow_diag_search_times(m._ctx, tl)
+                found_at["t"] = t_call + tl[7] / 1e9 if tl[7] >= 0 else time.perf_counter_ns() / 1e9
             return r
 
         def run_rank(nonce, n, rank, G, post_after_s=None, g=None):

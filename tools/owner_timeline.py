@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Host timeline of an 8-GPU node rank's search (tools/node_probe.py's owner, one GPU):
+where node_mine's time goes beyond the kernels.
+
+    python3 tools/owner_timeline.py > gpurun_out/<tag>/owner_timeline.json
+
+Per case (median of 7): node_mine's wall time; inside it, the time to the search call, the
+search call (Miner.search -> dpow_search), and after it; dpow_search's own timeline
+(dpow_diag_search_times: first launch planned, k = 0 kernel queued, first md5 launch
+queued, first completion record seen, done); the launches' kernel time from their records;
+and one plain Miner.search over the same window for comparison.  GPU box only."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "distributed-proof-of-work_amd"))
+import torch  # noqa: E402
+
+import distpow  # noqa: E402
+from distpow.node import BOARD_BATCH_CANDIDATES, NodeBoard, node_mine, owner_rank  # noqa: E402
+
+CASES = [([1, 2, 3, 4], 6, 2532284), ([1, 2, 3, 4], 7, 231910082), ([2, 2, 2, 2], 8, 293615578),
+         ([1, 2, 3, 4], 3, 97)]
+RUNS = 7
+
+
+def med(v):
+    return round(sorted(v)[len(v) // 2], 4)
+
+
+def main():
+    lib = distpow.lib()
+    board = NodeBoard.local()
+    out = {"build_id": distpow.build_id(), "cases": {}}
+    G = 8
+    with distpow.Miner(0) as m:
+        m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 26))  # warm
+        tl = (ctypes.c_int64 * 8)()
+        for nonce, n, g in CASES:
+            o = owner_rank(g, G)
+            rec = {"node_mine_ms": [], "to_search_ms": [], "search_ms": [], "after_ms": [], "kernel_ms": [],
+                   "launches": [], "dpow_timeline_us": [], "plain_search_ms": [], "plain_kernel_ms": []}
+            for _ in range(RUNS):
+                stamps = {}
+
+                def search(*a):
+                    stamps["s0"] = time.perf_counter()
+                    r = m.search(*a[:6], bound=a[6])
+                    stamps["s1"] = time.perf_counter()
+                    return r
+                torch.cuda.synchronize()
+                m.reset_stats()
+                t0 = time.perf_counter()
+                r = node_mine(search, nonce, n, o, G, board=board, attach_fn=m.attach_node)
+                t1 = time.perf_counter()
+                assert r.global_idx == g
+                st = m.stats()
+                lib.dpow_diag_search_times(m._ctx, tl)
+                rec["node_mine_ms"].append((t1 - t0) * 1e3)
+                rec["to_search_ms"].append((stamps["s0"] - t0) * 1e3)
+                rec["search_ms"].append((stamps["s1"] - stamps["s0"]) * 1e3)
+                rec["after_ms"].append((t1 - stamps["s1"]) * 1e3)
+                rec["kernel_ms"].append(st.kernel_ms)
+                rec["launches"].append(st.launches)
+                rec["dpow_timeline_us"].append([round(x / 1e3, 1) for x in tl])
+                # the same window as one plain search (no node_mine, no board)
+                rbits = 8 - 3
+                torch.cuda.synchronize()
+                m.reset_stats()
+                t0 = time.perf_counter()
+                r2 = m.search(nonce, n, o, 3, 0, BOARD_BATCH_CANDIDATES >> rbits)
+                rec["plain_search_ms"].append((time.perf_counter() - t0) * 1e3)
+                rec["plain_kernel_ms"].append(m.stats().kernel_ms)
+                assert r2.global_idx == g
+            key = f"G8 owner {bytes(nonce).hex()}/{n}"
+            out["cases"][key] = {k: (med(v) if k != "dpow_timeline_us" else v[len(v) // 2]) if k != "launches" else v[0]
+                                 for k, v in rec.items()}
+            print(key, json.dumps(out["cases"][key]), file=sys.stderr, flush=True)
+    out["note"] = ("dpow_timeline_us: [0] k0 queued, [1] first md5 queued, [2] first record seen, [3] done, "
+                   "[4] first launch planned, [5] k0 slot retired, [6] md5 slot retired (us from dpow_search's start)")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Per-wave timeline of one search launch (a diagnostic build with -DDPOW_WAVE_TRACE=1):
 where the fixed per-launch overhead goes (wave start spread, first-claim delay, exit spread).
-GPU box only:  DPOW_LIB_PATH=abx/libdpow_trace.so python3 tools/wave_trace.py"""
+GPU box only:  DPOW_LIB_PATH=distributed-proof-of-work_amd/distpow/libdpow_trace.so python3 tools/wave_trace.py"""
 import ctypes, json, os, sys
 sys.path.insert(0, "distributed-proof-of-work_amd")
 import distpow
 from distpow import _lib
 
 W = 6144  # worker waves of a full grid (6 four-wave workgroups per CU x 256 CUs)
+F = 8  # words per wave (md5_search_kernel.h kTraceFields)
 lib = ctypes.CDLL(_lib.LIB_PATH)
 m = distpow.Miner(0)
 m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 24))  # warm the clock
@@ -25,9 +26,9 @@ for wbits, wb in ((3, 5), (0, 0), (3, 5)):
     m.reset_stats()
     m.search([1, 2, 3, 4], 32, wb, wbits, k0, k0 + nk)
     st = m.stats()
-    buf = (ctypes.c_ulonglong * (4 * W))()
-    assert lib.dpow_diag_wave_trace(buf, 4 * W) == 0
-    t = [tuple(buf[4 * i:4 * i + 4]) for i in range(W)]
+    buf = (ctypes.c_ulonglong * (F * W))()
+    assert lib.dpow_diag_wave_trace(buf, F * W) == 0
+    t = [tuple(buf[F * i:F * i + 4]) for i in range(W)]
     os.makedirs("gpurun_out", exist_ok=True)
     with open(f"gpurun_out/wave_trace_{len(out)}_wbits{wbits}.json", "w") as f:
         json.dump(t, f)

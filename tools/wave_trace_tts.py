@@ -2,13 +2,14 @@
 """Per-wave timeline of the md5 launch of short time-to-secret searches (a diagnostic build
 with -DDPOW_WAVE_TRACE=1): where a launch whose hashing takes ~10 us spends the rest --
 wave start spread, first-claim delay, the spread of wave exits after the hit.
-GPU box only:  DPOW_LIB_PATH=abx/libdpow_trace.so python3 tools/wave_trace_tts.py"""
+GPU box only:  DPOW_LIB_PATH=distributed-proof-of-work_amd/distpow/libdpow_trace.so python3 tools/wave_trace_tts.py"""
 import ctypes, json, sys
 sys.path.insert(0, "distributed-proof-of-work_amd")
 import distpow
 from distpow import _lib
 
 W = 8192
+F = 8  # words per wave (md5_search_kernel.h kTraceFields)
 lib = ctypes.CDLL(_lib.LIB_PATH)
 m = distpow.Miner(0)
 m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 24))  # warm the clock
@@ -25,13 +26,13 @@ cases = {"mine_1234_N6": ([1, 2, 3, 4], 6, 0, 0, 0, 1 << 24), "mine_5678_N5": ([
 out = {}
 for rep in range(2):
     for name, args in cases.items():
-        buf = (ctypes.c_ulonglong * (4 * W))()
-        lib.dpow_diag_wave_trace_ls(buf, 4 * W)
+        buf = (ctypes.c_ulonglong * (F * W))()
+        lib.dpow_diag_wave_trace_ls(buf, F * W)
         m.reset_stats()
         r = m.search(*args)
         st = m.stats()
-        assert lib.dpow_diag_wave_trace_ls(buf, 4 * W) == 0
-        t = [tuple(buf[4 * i:4 * i + 4]) for i in range(W)]
+        assert lib.dpow_diag_wave_trace_ls(buf, F * W) == 0
+        t = [tuple(buf[F * i:F * i + 4]) for i in range(W)]
         t = [x for x in t if x[0]]
         t0 = min(x[0] for x in t)
         us = lambda v: round(v / 100.0, 2)  # 100 MHz ticks -> us

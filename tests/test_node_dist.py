@@ -402,3 +402,65 @@ def test_node_vote_shared_memory():
     finally:
         shm.close()
         shm.unlink()
+
+
+def _worker_board_fail(rank, world, port, out_q):
+    """rank 0 cannot create the shared-memory segment (e.g. /dev/shm full):
+    every rank returns None from NodeBoard.create together, at once, instead of the
+    others waiting in broadcast_object_list until the process-group timeout."""
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+    from multiprocessing import shared_memory
+
+    import torch.distributed as dist
+    from distpow.node import NodeBoard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    if rank == 0:
+        class _Full:
+            def __init__(self, *a, **k):
+                raise OSError(28, "No space left on device")
+        shared_memory.SharedMemory = _Full
+    t0 = time.perf_counter()
+    board = NodeBoard.create()
+    out_q.put((rank, board is None, time.perf_counter() - t0))
+    dist.barrier()  # the group is still in step
+    dist.destroy_process_group()
+
+
+def test_board_creation_failure_is_agreed():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_board_fail, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(none for _, none, _ in outs), outs
+    assert all(dt < 10.0 for _, _, dt in outs), outs
+
+
+def test_board_without_attach_keeps_expected_time_batches():
+    """BOARD_BATCH_CANDIDATES (2^33 per rank: the board stops the kernels at the
+    first hit) only when attach_fn attaches the slot to the rank's search context; a board
+    without attach_fn gets node_mine's expected-time batch (auto_batch_candidates)."""
+    from distpow.node import BOARD_BATCH_CANDIDATES, NodeBoard, auto_batch_candidates, node_mine
+    board = NodeBoard.local()
+    wins = []
+
+    def search(nonce, ntz, wb, wbits, k0, k1, bound):
+        from distpow.search import SearchResult
+        wins.append(k1 - k0)
+        return SearchResult(0)  # EXHAUSTED
+
+    world, rank, n = 8, 3, 7
+    node_mine(search, [1, 2, 3, 4], n, rank, world, k_limit=1 << 30, board=board)
+    assert wins[0] == max(1, auto_batch_candidates(n, world) >> 5)
+    wins.clear()
+    node_mine(search, [1, 2, 3, 4], n, rank, world, k_limit=1 << 30, board=board, attach_fn=lambda s: None)
+    assert wins[0] == min(BOARD_BATCH_CANDIDATES >> 5, 1 << 30)

@@ -131,7 +131,8 @@ struct Launch {
     uint64_t n_static;     // claims [0, n_static) are handed out by wave index, not by a counter: worker
                            //  wave w's first claim is w (the "_ls" kernels only; 0 for every other launch)
     uint32_t poll_wb;      // wave-blocks per group: a wave reads Ctrl::best / Ctrl::stop once per group
-    uint32_t pad0;
+    uint32_t fair_ticks;   // fair priority (one-block kernels, DPOW_FAIR_PRIO): s_memrealtime ticks per wave-block
+                           //  at a fair share of the device, x 1.25; a wave behind that hashes at priority 2
     unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;              // this search's control block (clean at its first launch)

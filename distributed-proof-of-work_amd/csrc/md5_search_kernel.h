@@ -125,6 +125,17 @@ namespace DPOW_KNS {
 #ifndef DPOW_CLAIM_FRESH
 #define DPOW_CLAIM_FRESH 0
 #endif
+// Fair priority (one-block kernels): the SIMD's arbiter issues its oldest wave first, so the
+// youngest waves of a grid progress at a fraction of the others' rate, and the chunks they
+// hold delay a first hit and the drain behind it.  With it a wave compares the wave-blocks it
+// has hashed with what a fair share of the device would have hashed since it started
+// (Launch::fair_ticks per wave-block, from s_memrealtime) at each poll group, and hashes at
+// priority 2 while it is behind.  (A first version compared the chunk with its counter's
+// frontier, read with every poll group; those loads of the claim counters' lines slowed the
+// claims and an 8-GPU rank's N = 8 search 2.5x.)
+#ifndef DPOW_FAIR_PRIO
+#define DPOW_FAIR_PRIO 0
+#endif
 #ifndef DPOW_CLAIM_DEFER
 #define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch;
                             // one final block only, search_body kDeferClaims)
@@ -998,6 +1009,15 @@ DPOW_DEV void search_body(const Launch &L) {
     constexpr bool kDeferClaims = DPOW_CLAIM_DEFER && NBLK == 1;
     constexpr bool kLate = DPOW_CLAIM_LATE && kDeferClaims && DPOW_POLL_WB > 0;
     constexpr bool kFresh = DPOW_CLAIM_FRESH && NBLK == 1;
+    constexpr bool kFair = DPOW_FAIR_PRIO && NBLK == 1 && DPOW_POLL_WB > 0 && DPOW_TAIL_PRIO && !DPOW_HEAD_PRIO;
+    // kFair: the wave's start (s_memrealtime) and its wave-blocks, in VGPRs (wave-uniform; an
+    // SGPR live across the hash loop costs spill reloads inside it)
+    uint32_t fair_t0_v = 0, fair_wb_v = 0;
+    if constexpr (kFair) {
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        asm volatile("v_mov_b32 %0, %1" : "=v"(fair_t0_v) : "s"(t0));
+        asm volatile("v_mov_b32 %0, 0" : "=v"(fair_wb_v));
+    }
     uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
 #if DPOW_STATIC_FIRST
@@ -1090,6 +1110,7 @@ DPOW_DEV void search_body(const Launch &L) {
         const uint32_t poll_wb = kLaunchPoll<NBLK, W0, SH> ? L.poll_wb : (uint32_t)DPOW_POLL_WB;
         for (;;) {
             uint32_t q = left < poll_wb ? left : poll_wb;
+            [[maybe_unused]] const uint32_t q0 = q;  // (kFair: wave-blocks of this group)
 #if DPOW_SPAN
             // A chunk never straddles a 2^24-k segment boundary (the host aligns a
             // spanning launch's chunks to them, dpow_api.cpp), so neither does a
@@ -1138,6 +1159,17 @@ DPOW_DEV void search_body(const Launch &L) {
             }
             best = best_seen < best ? best_seen : best;
             stop = stop_seen;
+            if constexpr (kFair) {
+                // behind a fair share of the device since this wave started: priority 2 (big claims;
+                // the tail's claims stay at 0, tail priority)
+                const uint32_t done_wb = __builtin_amdgcn_readfirstlane(fair_wb_v) + (q0 - q);
+                asm volatile("v_mov_b32 %0, %1" : "=v"(fair_wb_v) : "s"(done_wb));
+                const uint32_t el = (uint32_t)__builtin_amdgcn_s_memrealtime() - __builtin_amdgcn_readfirstlane(fair_t0_v);
+                if (claim < L.n_big) {
+                    if (el > (done_wb + 2u) * L.fair_ticks) __builtin_amdgcn_s_setprio(2);
+                    else __builtin_amdgcn_s_setprio(1);
+                }
+            }
             if (hit || left == 0 || stop != 0u || global_of_local(i0, L.rbits, L.base_tb) >= best) break;
         }
 #else

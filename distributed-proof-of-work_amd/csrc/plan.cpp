@@ -332,6 +332,11 @@ int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t s
                                knobs.cpw ? knobs.cpw : launch_claims_per_wave(ntz, L.rbits));
     if (rc < 0) return rc;
     L.poll_wb = knobs.poll_wb ? knobs.poll_wb : launch_poll_wb(ntz, L.rbits);
+    // Fair priority (md5_search_kernel.h DPOW_FAIR_PRIO): s_memrealtime ticks (100 MHz) per
+    // wave-block of a wave at a fair share of the device -- waves x 128 candidates / kFairRate --
+    // with 25 % slack.
+    const double waves = (double)*worker_blocks * (kBlockThreads / 64);
+    L.fair_ticks = (uint32_t)std::max(1.0, 1.25 * waves * (double)kWaveBlock / kFairRate * 1e8);
     return 0;
 }
 

@@ -167,6 +167,7 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits)
 // counter), size_launch with the ntz-dependent expected first hit, minimum chunk and
 // claims per wave, and the poll group (L.poll_wb).  Non-zero knobs override the policy
 // (the DPOW_DIAG_* A/B environment of dpow_open).
+constexpr double kFairRate = 2.05e11;  // candidates/s of a device at 4-6 workgroups per CU (one block)
 struct LaunchKnobs {
     uint32_t bpc = 0, min_chunk = 0, cpw = 0, poll_wb = 0;
 };

@@ -81,6 +81,13 @@ def summarize(before, after):
                         "last_chunk_start_us": us(x[4] - t0) if x[4] else None, "wblocks": x[3], "reason": x[6]}
                        for x in last],
         "chunk_of_first_hit": min((x for x in t if x[7]), key=lambda x: x[7])[5] if hits else None,
+        # the wave that found the first hit: when it started the hit's chunk, its wave-blocks,
+        # and where it stood among all waves (its wave-blocks' rank, 0 = fewest)
+        "hit_wave": (lambda x: {"start_us": us(x[0] - t0), "hit_chunk_start_us": us(x[4] - t0),
+                                "hit_us": us(x[7] - t0), "wblocks": x[3],
+                                "wblocks_rank": sum(1 for y in t if y[3] < x[3]) / len(t)})(
+            min((x for x in t if x[7]), key=lambda x: x[7])) if hits else None,
+        "wblocks_p0_p10_p50": [min(x[3] for x in t), pct([x[3] for x in t], .1), pct([x[3] for x in t], .5)],
     }
 
 

@@ -113,8 +113,11 @@ namespace DPOW_KNS {
 // kernels): a wave then reserves its next chunk only near the end of the current one, so a
 // slow wave does not sit on an early chunk for the whole of its current one, and the polls of
 // the chunk's earlier groups do not wait for the claim atomic (vmcnt counts in issue order).
+// Round 4, five same-box A/Bs of the sweep (tools/ab_variants.py, profiles/r04_node_ab.log):
+// +0.03 to +0.24 % (218.15-218.95 against 217.91-218.48 GH/s); an 8-GPU rank's
+// [2,2,2,2]/8 0.358-0.374 against 0.376-0.378 ms, the other node cases within noise.
 #ifndef DPOW_CLAIM_LATE
-#define DPOW_CLAIM_LATE 0
+#define DPOW_CLAIM_LATE 1
 #endif
 // A fresh read of Ctrl::best / Ctrl::stop at the end of each chunk (one-block kernels), for
 // the check at the next claim: the group's poll was issued at the group's start, so a wave

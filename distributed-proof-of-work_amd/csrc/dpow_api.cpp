@@ -854,21 +854,66 @@ int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, u
 
 int dpow_diag_node_post_at(dpow_node_slot *slot, uint64_t global_idx, int64_t t_ns) {
     if (!slot) return set_error(DPOW_EINVAL, "dpow_diag_node_post_at: slot is NULL");
-    std::thread([slot, global_idx, t_ns]() {
-        for (;;) {
-            struct timespec ts;
-            clock_gettime(CLOCK_MONOTONIC, &ts);
-            const int64_t left = t_ns - ((int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec);
-            if (left <= 0) break;
-            if (left > 100000) {
-                const struct timespec d = {0, (long)(left - 50000)};
-                nanosleep(&d, nullptr);
-            } else {
-                __builtin_ia32_pause();
+    // One poster thread per process, spinning while requests may come (it exits after 2 s
+    // without one): queueing a request costs the caller a lock, not a thread creation --
+    // round 3 started a thread per post, on the emulated rank's clock.  The state is never
+    // destroyed (the detached thread may still run while the process exits).
+    struct Poster {
+        std::mutex mu;
+        std::vector<std::pair<int64_t, std::pair<dpow_node_slot *, uint64_t>>> q;
+        std::atomic<int> pending{0};
+        bool alive = false;
+    };
+    static Poster *const P = new Poster;
+    std::lock_guard<std::mutex> g(P->mu);
+    P->q.push_back({t_ns, {slot, global_idx}});
+    P->pending.fetch_add(1, std::memory_order_release);
+    if (!P->alive) {
+        P->alive = true;
+        std::thread([]() {
+            auto mono = []() {
+                struct timespec ts;
+                clock_gettime(CLOCK_MONOTONIC, &ts);
+                return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+            };
+            int64_t idle_since = mono();
+            for (;;) {
+                if (P->pending.load(std::memory_order_acquire) == 0) {
+                    if (mono() - idle_since > 2000000000) {
+                        std::lock_guard<std::mutex> g2(P->mu);
+                        if (P->pending.load(std::memory_order_acquire) == 0) {
+                            P->alive = false;
+                            return;
+                        }
+                    }
+                    __builtin_ia32_pause();
+                    continue;
+                }
+                std::vector<std::pair<int64_t, std::pair<dpow_node_slot *, uint64_t>>> work;
+                {
+                    std::lock_guard<std::mutex> g2(P->mu);
+                    work.swap(P->q);
+                    P->pending.fetch_sub((int)work.size(), std::memory_order_acq_rel);
+                }
+                std::sort(work.begin(), work.end(),
+                          [](const auto &x, const auto &y) { return x.first < y.first; });
+                for (const auto &w : work) {
+                    for (;;) {
+                        const int64_t left = w.first - mono();
+                        if (left <= 0) break;
+                        if (left > 100000) {
+                            const struct timespec d = {0, (long)(left - 50000)};
+                            nanosleep(&d, nullptr);
+                        } else {
+                            __builtin_ia32_pause();
+                        }
+                    }
+                    dpow_node_post(w.second.first, w.second.second);
+                }
+                idle_since = mono();
             }
-        }
-        dpow_node_post(slot, global_idx);
-    }).detach();
+        }).detach();
+    }
     return 0;
 }
 

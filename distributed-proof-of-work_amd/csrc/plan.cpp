@@ -311,6 +311,7 @@ uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits) {
     const uint32_t slow = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 16;
     const uint64_t expect = expected_first_hit(ntz, rbits);
     if (DPOW_SMALL_GRIDS && expect <= kTinyExpect) return 1;
+    if (DPOW_SMALL_GRIDS && expect <= kMidExpect) return kMidPollWb;
     return expect <= kFastPollCands ? kFastPollWb : slow;
 }
 
@@ -319,7 +320,9 @@ uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits) {
 }
 
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits) {
-    return DPOW_SMALL_GRIDS && expected_first_hit(ntz, rbits) <= kTinyExpect ? kTinyChunk : kMinChunk;
+    const uint64_t expect = expected_first_hit(ntz, rbits);
+    if (DPOW_SMALL_GRIDS && expect <= kTinyExpect) return kTinyChunk;
+    return DPOW_SMALL_GRIDS && expect > kMidChunkExpect && expect <= kMidExpect ? kMidChunk : kMinChunk;
 }
 
 int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t share, const LaunchKnobs &knobs,

@@ -105,10 +105,18 @@ uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits);
 #ifndef DPOW_POLL_WB
 #define DPOW_POLL_WB 16  // (also md5_search_kernel.h)
 #endif
+// Round 4 (the early Found fan-out, the claim-ahead in a chunk's last group): searches
+// expected beyond kMidExpect poll every 8 wave-blocks (round 3: 4), those up to it every 4.
+// An 8-GPU node, emulated (tools/node_probe.py, profiles/r04_node_ab.log r04ab6): [2,2,2,2]/8
+// 0.354 -> 0.323 ms, [1,2,3,4]/8 2.67 -> 2.63 ms with every launch at 8.
 #ifndef DPOW_FAST_POLL_WB
-#define DPOW_FAST_POLL_WB 4
+#define DPOW_FAST_POLL_WB 8
+#endif
+#ifndef DPOW_MID_POLL_WB
+#define DPOW_MID_POLL_WB 4
 #endif
 constexpr uint32_t kFastPollWb = DPOW_FAST_POLL_WB;
+constexpr uint32_t kMidPollWb = DPOW_MID_POLL_WB;
 constexpr uint64_t kFastPollCands = 1ull << 30;
 uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
 // Tiny searches -- a first hit expected within kTinyExpect candidates of the partition (N <= 5
@@ -137,6 +145,18 @@ constexpr uint64_t kMidExpect = 1ull << 26;
 #endif
 constexpr uint64_t kFiveExpect = DPOW_FIVE_EXPECT_LOG2 ? 1ull << DPOW_FIVE_EXPECT_LOG2 : 0;
 constexpr uint64_t kTinyChunk = 2;
+// Claims of at least kMidChunk wave-blocks for hits expected in (kMidChunkExpect, kMidExpect]
+// (round 3: kMinChunk = 4): half the claims, and with the claim-ahead in a chunk's last group
+// the chunk's first group polls without waiting for the claim atomic.  Emulated 8-GPU node
+// (profiles/r04_node_ab.log r04ab7): [1,2,3,4]/7 0.266-0.270 -> 0.251-0.261 ms, its owner
+// 0.217-0.223 -> 0.196-0.204 ms.  Not below: every wave's first two claims at 4 per CU and
+// 8 wave-blocks cover 2^23 candidates, and a hit inside them waits for its larger chunk
+// (one GPU's [1,2,3,4]/6, 2^24 expected: 0.064-0.075 -> 0.079-0.082 ms with chunks of 8).
+#ifndef DPOW_MID_CHUNK
+#define DPOW_MID_CHUNK 8
+#endif
+constexpr uint64_t kMidChunk = DPOW_MID_CHUNK;
+constexpr uint64_t kMidChunkExpect = 1ull << 24;
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits);
 // Claims per wave (chunk sizing) of a search expected to end within kFastPollCands
 // candidates: 64 (smaller chunks), else kClaimsPerWave.  A rank that another rank's hit stops

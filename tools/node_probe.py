@@ -88,15 +88,19 @@ def main():
                 found_at["t"] = t_call + tl[7] / 1e9 if tl[7] >= 0 else time.perf_counter_ns() / 1e9
             return r
 
+        warm = NodeBoard.local()
+
         def run_rank(nonce, n, rank, G, post_after_s=None, g=None):
             slot = board.begin()
+            lib.dpow_diag_node_post_at(warm.slot(0), 0, 0)  # the poster thread running before the clock
             torch.cuda.synchronize()
             found_at.clear()
             t0 = time.perf_counter_ns()  # CLOCK_MONOTONIC
             if post_after_s is not None:
                 # the owner's process posts its hit at t0 + post_after_s: a native thread, off
                 # this interpreter (a Python poster thread took the GIL and its start alone
-                # cost the rank 50-100 us)
+                # cost the rank 50-100 us; round 3 created a native thread per post, on the
+                # clock; now one queues a request for a poster already running)
                 lib.dpow_diag_node_post_at(slot, g, t0 + int(post_after_s * 1e9))
             res = node_mine(search_timed, nonce, n, rank, G, board=board, attach_fn=m.attach_node)
             dt = (time.perf_counter_ns() - t0) / 1e9

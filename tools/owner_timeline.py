@@ -34,6 +34,7 @@ def med(v):
 def main():
     lib = distpow.lib()
     board = NodeBoard.local()
+    warm = NodeBoard.local()
     out = {"build_id": distpow.build_id(), "cases": {}}
     G = 8
     with distpow.Miner(0) as m:
@@ -79,8 +80,48 @@ def main():
             out["cases"][key] = {k: (med(v) if k != "dpow_timeline_us" else v[len(v) // 2]) if k != "launches" else v[0]
                                  for k, v in rec.items()}
             print(key, json.dumps(out["cases"][key]), file=sys.stderr, flush=True)
+            # a non-owner, the owner's hit posted to its slot when the owner posted it (node_probe.py)
+            t_post = med([a + b / 1e3 for a, b in zip(rec["to_search_ms"],
+                                                      [tl_[7] if tl_[7] >= 0 else 1e9 for tl_ in rec["dpow_timeline_us"]])])
+            non = (o + 1) % G
+            nrec = {"node_mine_ms": [], "to_search_ms": [], "search_ms": [], "after_ms": [], "kernel_ms": [],
+                    "launches": [], "dpow_timeline_us": []}
+            for _ in range(RUNS):
+                stamps = {}
+
+                def search2(*a):
+                    stamps["s0"] = time.perf_counter()
+                    r = m.search(*a[:6], bound=a[6])
+                    stamps["s1"] = time.perf_counter()
+                    return r
+                slot = board.begin()
+                lib.dpow_diag_node_post_at(warm.slot(0), 0, 0)  # the poster thread running before the clock
+                torch.cuda.synchronize()
+                m.reset_stats()
+                t0 = time.perf_counter()
+                lib.dpow_diag_node_post_at(slot, g, time.perf_counter_ns() + int(t_post * 1e6))
+                t0b = time.perf_counter()
+                r = node_mine(search2, nonce, n, non, G, board=board, attach_fn=m.attach_node)
+                t1 = time.perf_counter()
+                assert r.global_idx == g
+                st = m.stats()
+                lib.dpow_diag_search_times(m._ctx, tl)
+                nrec["node_mine_ms"].append((t1 - t0) * 1e3)
+                nrec["to_search_ms"].append((stamps["s0"] - t0) * 1e3)
+                nrec["search_ms"].append((stamps["s1"] - stamps["s0"]) * 1e3)
+                nrec["after_ms"].append((t1 - stamps["s1"]) * 1e3)
+                nrec["kernel_ms"].append(st.kernel_ms)
+                nrec["launches"].append(st.launches)
+                nrec["dpow_timeline_us"].append([round(x / 1e3, 1) for x in tl] + [round((t0b - t0) * 1e6, 1)])
+            key = f"G8 non-owner {bytes(nonce).hex()}/{n}"
+            out["cases"][key] = {k: (med(v) if k != "dpow_timeline_us" else v[len(v) // 2]) if k != "launches" else v[0]
+                                 for k, v in nrec.items()}
+            out["cases"][key]["post_ms"] = round(t_post, 4)
+            print(key, json.dumps(out["cases"][key]), file=sys.stderr, flush=True)
     out["note"] = ("dpow_timeline_us: [0] k0 queued, [1] first md5 queued, [2] first record seen, [3] done, "
-                   "[4] first launch planned, [5] k0 slot retired, [6] md5 slot retired (us from dpow_search's start)")
+                   "[4] first launch planned, [5] k0 slot retired, [6] md5 slot retired, [7] early hit posted "
+                   "(us from dpow_search's start); non-owner: [8] the poster thread's creation (us); post_ms: "
+                   "the owner's post, from its node_mine start")
     print(json.dumps(out, indent=1))
 
 

@@ -155,9 +155,11 @@ struct SearchWait {
     // Ctrl::best to, the lowest value seen there, and what a hit is verified against.
     const uint64_t *early = nullptr;
     uint64_t early_seen = DPOW_NO_HIT;
+    uint64_t own_posted = DPOW_NO_HIT;  // the lowest hit of ours posted early: the slot's best, not a bound
     const uint8_t *nonce = nullptr;
     size_t nonce_len = 0;
     uint32_t ntz = 0;
+    uint32_t rbits = 8, base_tb = 0;    // the partition: g is ours iff (g & 255) >> rbits == base_tb >> rbits
     void lower_slack() {
         if (old_slack >= 0) return;
         // Linux pads a normal thread's nanosleep by its 50 us default timer slack,
@@ -238,7 +240,9 @@ int poll_node(dpow_ctx *c, SearchWait &sw) {
     if (nb < sw.node_seen) {
         // The running launch's watcher lowers Ctrl::best to it on the device; the host
         // keeps the injected bound (ext_bound) that tells another rank's index from ours.
+        // Our own hit, posted early (poll_early), is not a bound.
         sw.node_seen = nb;
+        if (nb == sw.own_posted) return 0;
         std::lock_guard<std::mutex> g(c->bound_mu);
         uint64_t cur = c->ext_bound.load(std::memory_order_relaxed);
         if (nb < cur) c->ext_bound.store(nb, std::memory_order_release);
@@ -258,10 +262,13 @@ void poll_early(dpow_ctx *c, SearchWait &sw) {
     const uint64_t g = __atomic_load_n(sw.early, __ATOMIC_ACQUIRE);
     if (g >= sw.early_seen) return;
     sw.early_seen = g;
+    // only a hit of this search's partition (Ctrl::best also holds the bounds the watcher relays)
+    if ((((uint32_t)g & 0xFFu) >> sw.rbits) != (sw.base_tb >> sw.rbits)) return;
     uint8_t sec[DPOW_MAX_SECRET];
     size_t len = 0;
     if (dpow_secret_from_index(g, sec, &len) != 0) return;
-    if (!dpow_verify(sw.nonce, sw.nonce_len, sec, len, sw.ntz)) return;  // never expected: left to the record
+    if (!dpow_verify(sw.nonce, sw.nonce_len, sec, len, sw.ntz)) return;  // not a hit (a bound): left to the record
+    if (g < sw.own_posted) sw.own_posted = g;  // before the post: poll_node must not take it for a bound
     dpow_node_post(c->node, g);
     if (c->diag_t[7] < 0) c->diag_t[7] = now_ns() - sw.t0;
 }
@@ -360,6 +367,8 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         sw.nonce = nonce;
         sw.nonce_len = nonce_len;
         sw.ntz = ntz;
+        sw.rbits = remainder_bits(worker_bits);
+        sw.base_tb = base_thread_byte(worker_byte, worker_bits);
     }
     size_t launched = 0, consumed = 0;
     int64_t busy_until = 0;  // expected end of the launches queued so far (now_ns clock)

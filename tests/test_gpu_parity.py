@@ -660,6 +660,37 @@ def test_two_contexts_share_a_slot_one_closes(miner, golden):
     assert r.status == FOUND and r.global_idx == e["global_idx"]
 
 
+def test_early_found_fan_out(miner, golden):
+    """Round 4: a search attached to a node slot posts its verified hit to the slot while its
+    launch still drains (the watcher relays Ctrl::best to a pinned word, the searching thread
+    verifies and posts it: dpow_diag_search_times[7]), before the search returns ([3]); the
+    posted value is the search's own answer, and a bound that is not a hit (posted by the
+    test) is never taken for one.  Partition case: workerBits 3, the owner of [1,2,3,4]/7."""
+    e = next(x for x in golden["first_hits"] if x["nonce"] == [1, 2, 3, 4] and x["ntz"] == 7)
+    g = e["global_idx"]
+    wb = (g & 0xFF) >> 5
+    slot = _Slot()
+    addr = ctypes.addressof(slot)
+    lib = distpow.lib()
+    tl = (ctypes.c_int64 * 8)()
+    miner.attach_node(addr)
+    try:
+        for _ in range(3):
+            lib.dpow_node_slot_reset(addr)
+            r = miner.search([1, 2, 3, 4], 7, wb, 3, 0, 1 << 24)
+            assert r.status == FOUND and r.global_idx == g
+            assert slot.best == g
+            lib.dpow_diag_search_times(miner._ctx, tl)
+            assert 0 <= tl[7] < tl[3], list(tl)
+        # a bound that is no hit, above the answer: still our hit, and nothing else posted
+        lib.dpow_node_slot_reset(addr)
+        lib.dpow_node_post(addr, g + 3)
+        r = miner.search([1, 2, 3, 4], 7, wb, 3, 0, 1 << 24)
+        assert r.status == FOUND and r.global_idx == g and slot.best == g
+    finally:
+        miner.attach_node(None)
+
+
 def test_concurrent_searches_share_the_gpu(golden):
     """Four contexts searching at once on one GPU (each sizes its grids to its share of the
     device, dpow_api.cpp ActiveSearch): every answer is still the golden, and a concurrent

@@ -221,20 +221,28 @@ DPOW_DEV_CONST bool seg_word(int m) {
 #endif
 constexpr int pipe_lead(int nblk, int w0, int sh) {
     if (DPOW_PIPE_LEAD > 0) return DPOW_PIPE_LEAD;
+    // (round 4: the same sweep over the round-4 kernels, profiles/r04_lead_sweep.json, moved the
+    // entries marked r4 -- a start that beats the table's by >= 1 % -- and dropped <1,10,1..2>'s
+    // 3, now 7.4 % below 4)
     if (nblk == 1) {
         switch (w0 * 4 + sh) {
             case 0 * 4 + 0: return 2;  // +1.3 %
+            case 0 * 4 + 3: return 2;  // r4 +1.1 %
             case 2 * 4 + 0: return 3;  // +2.0 %
-            case 2 * 4 + 1: return 2;  // +0.8 %
-            case 2 * 4 + 2: return 2;  // +0.9 %
+            case 2 * 4 + 1: return 1;  // r4 +1.2 % (round 2: 2)
+            case 2 * 4 + 2: return 1;  // r4 +1.2 % (round 2: 2)
             case 3 * 4 + 0: return 3;  // +2.2 %
+            case 3 * 4 + 1: return 3;  // r4 +1.2 %
+            case 3 * 4 + 2: return 3;  // r4 +1.1 %
             case 3 * 4 + 3: return 1;  // +2.0 %
+            case 4 * 4 + 0: return 2;  // r4 +1.5 %
             case 4 * 4 + 3: return 2;  // +1.0 %
+            case 6 * 4 + 3: return 2;  // r4 +1.4 %
             case 8 * 4 + 3: return 3;  // +2.2 %
             case 9 * 4 + 0: return 2;  // +3.7 %
+            case 9 * 4 + 1: return 3;  // r4 +2.3 %
+            case 9 * 4 + 2: return 3;  // r4 +2.3 %
             case 9 * 4 + 3: return 3;  // +1.6 %
-            case 10 * 4 + 1: return 3; // +0.8 %
-            case 10 * 4 + 2: return 3; // +1.0 %
             case 10 * 4 + 3: return 5; // +1.8 %
             default: return 4;
         }
@@ -245,6 +253,8 @@ constexpr int pipe_lead(int nblk, int w0, int sh) {
         case 14 * 4 + 2: return 2;  // +5.1 %
         case 14 * 4 + 3: return 1;  // +4.3 %
         case 15 * 4 + 0: return 2;  // +4.5 %
+        case 15 * 4 + 1: return 2;  // r4 +2.2 %
+        case 15 * 4 + 2: return 2;  // r4 +2.3 %
         case 15 * 4 + 3: return 1;  // +5.7 %
         default: return 4;
     }
@@ -292,7 +302,11 @@ struct VgprK {
     // The segment-word constants count against them first.  Round 1's caps for
     // <= 64 VGPRs (14 one-block / 10 two-block for SH != 0) left the two-block
     // layouts with 4-11 SGPR spill reloads per wave-block.
+    // (round 4, profiles/r04_lead_sweep.json: a cap of 24 for <1,7,1..2> +1.9-2.0 %,
+    // <1,4,3> +1.5 %, <1,5,3> +1.0 %; elsewhere it is no better, or costs up to 3 %)
+    static constexpr bool kCap24 = NBLK == 1 && ((W0 == 7 && (SH == 1 || SH == 2)) || (SH == 3 && (W0 == 4 || W0 == 5)));
     static constexpr int kCap = DPOW_VGPR_K_MAX >= 0 ? DPOW_VGPR_K_MAX
+                                : kCap24 ? 24
                                 : NBLK == 1 ? (SH == 0 ? 24 : SH == 3 ? 14 : 18)
                                             : (SH == 3 ? 20 : 26);
     static constexpr bool use(int blk, int i) {
@@ -935,13 +949,16 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
 // 4-41 per wave-block; 0 at 96).
 // The two-block W0 = 15 layouts get 100 (DPOW_NUM_SGPR_W15): at 96 three of them kept 3
 // spill reloads per wave-block in every launch-field choice (kLaunchPoll), at 100 they keep
-// 0-1; for the other two-block layouts 100 is no better than 96.  7 waves still fit.
+// 0-1.  Round 4's per-layout sweep of a 100 budget for every long layout (tools/lead_sweep.py,
+// profiles/r04_lead_sweep.json) added <2,13,3> (+1.5 %), <2,14,3> (+0.7 %) and <1,11,3>
+// (+2.6 %); elsewhere 100 is within +-0.3 % of 96.  7 waves still fit.
 // (The attribute takes no template-dependent value: three kernel templates share
 // one body, and md5_variant.hip instantiates the one kLongSgpr / kW15Sgpr select.)
 template <int NBLK, int W0>
 constexpr bool kLongSgpr = NBLK == 2 || W0 >= DPOW_SGPR_LONG_W0;
-template <int NBLK, int W0>
-constexpr bool kW15Sgpr = NBLK == 2 && W0 == 15;
+template <int NBLK, int W0, int SH>
+constexpr bool kW15Sgpr = (NBLK == 2 && W0 == 15) || (NBLK == 2 && SH == 3 && (W0 == 13 || W0 == 14)) ||
+                          (NBLK == 1 && W0 == 11 && SH == 3);
 
 // Whether a kernel reads the poll group (Launch::poll_wb) and the next search's control block
 // (Launch::ctrl_next) from the launch, or uses the compile-time group and derives the block in

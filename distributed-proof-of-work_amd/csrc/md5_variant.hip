@@ -23,10 +23,10 @@ using KernelFn = void (*)(Launch);
 // one final block only.
 // The kernel of a layout: the long-SGPR-budget template for long nonces and two
 // final blocks (md5_search_kernel.h kLongSgpr), a slightly larger budget for the two-block
-// W0 = 15 layouts (kW15Sgpr); only the chosen one is instantiated.
+// W0 = 15 layouts and a few more (kW15Sgpr); only the chosen one is instantiated.
 template <int NBLK, int W0, int SH, bool EQ>
 constexpr KernelFn kernel_of() {
-    if constexpr (kW15Sgpr<NBLK, W0>) return md5_search_kernel_w15sgpr<NBLK, W0, SH, EQ>;
+    if constexpr (kW15Sgpr<NBLK, W0, SH>) return md5_search_kernel_w15sgpr<NBLK, W0, SH, EQ>;
     else if constexpr (kLongSgpr<NBLK, W0>) return md5_search_kernel_lsgpr<NBLK, W0, SH, EQ>;
     else return md5_search_kernel<NBLK, W0, SH, EQ>;
 }

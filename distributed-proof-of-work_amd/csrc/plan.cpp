@@ -311,6 +311,7 @@ uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits) {
     const uint32_t slow = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 16;
     const uint64_t expect = expected_first_hit(ntz, rbits);
     if (DPOW_SMALL_GRIDS && expect <= kTinyExpect) return 1;
+    if (DPOW_SMALL_GRIDS && expect <= kNearExpect) return kNearPollWb;
     if (DPOW_SMALL_GRIDS && expect <= kMidExpect) return kMidPollWb;
     return expect <= kFastPollCands ? kFastPollWb : slow;
 }

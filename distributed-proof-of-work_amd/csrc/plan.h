@@ -115,8 +115,17 @@ uint64_t expected_first_hit(uint32_t ntz, uint32_t rbits);
 #ifndef DPOW_MID_POLL_WB
 #define DPOW_MID_POLL_WB 4
 #endif
+// Hits expected within kNearExpect (2^24: one GPU's N = 6, a 2- or 4-GPU rank's N = 6) often lie among the chunks every wave claims first, and the waves above
+// the hit hash a whole group before they see it: groups of 2 (round 4,
+// profiles/r04_small_probe/: one GPU's [1,2,3,4]/6 0.064-0.073 -> 0.052-0.053 ms at 4 per
+// CU; over 24 fresh nonces at N = 6 0.137-0.138 -> 0.141-0.143 ms).
+#ifndef DPOW_NEAR_POLL_WB
+#define DPOW_NEAR_POLL_WB 2
+#endif
+constexpr uint64_t kNearExpect = 1ull << 24;
 constexpr uint32_t kFastPollWb = DPOW_FAST_POLL_WB;
 constexpr uint32_t kMidPollWb = DPOW_MID_POLL_WB;
+constexpr uint32_t kNearPollWb = DPOW_NEAR_POLL_WB;
 constexpr uint64_t kFastPollCands = 1ull << 30;
 uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
 // Tiny searches -- a first hit expected within kTinyExpect candidates of the partition (N <= 5
@@ -126,8 +135,13 @@ uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
 // of a lightly loaded SIMD finishes a wave-block sooner.  Measured over the BASELINE cases
 // and 24 fresh nonces each (tools/small_search_probe.py, profiles/r03_small_probe.json):
 // [5,6,7,8]/5 0.040 -> 0.025 ms, fresh N = 5 0.044 -> 0.035 ms, an 8-GPU rank's
-// [1,2,3,4]/6 0.043 -> 0.026 ms.
-constexpr uint64_t kTinyExpect = 1ull << 21;
+// [1,2,3,4]/6 0.043 -> 0.026 ms.  (Round 4 tried ending the tier at 2^20, moving an 8-GPU
+// rank's N = 6 to 3 workgroups per CU and claims of 4: the emulated node's [1,2,3,4]/6 went
+// 0.046 -> 0.056 ms, profiles/r04_small_probe/; not kept.)
+#ifndef DPOW_TINY_EXPECT_LOG2
+#define DPOW_TINY_EXPECT_LOG2 21
+#endif
+constexpr uint64_t kTinyExpect = 1ull << DPOW_TINY_EXPECT_LOG2;
 // Up to kMidExpect (N = 6 on one GPU, N = 7 on a rank of a 4- or 8-GPU node): 4 workgroups
 // per CU.  The rate is ~6 % below the full grid's, but a rank that another rank's hit
 // stops drains in half the time: stop latency at N = 7 on an 8-GPU rank's window 103 ->

@@ -166,7 +166,7 @@ def test_chunk_length_spanning_launches(ntz):
             assert len(ds) == 2 and ds[0].k_end == le
         for d in ds:
             check(d, grid_cap(cus, share))
-            assert d.poll_wb in (1, 4, 8, 16)
+            assert d.poll_wb in (1, 2, 4, 8, 16)
 
 
 def test_bench_step_is_one_launch():
@@ -183,7 +183,8 @@ def test_short_search_grids():
     own sizing): an 8-GPU rank's N = 6 window gets 2 workgroups per CU, claims of 2
     wave-blocks, a poll after every wave-block and static first claims; one GPU's N = 7 5
     workgroups per CU with 8-wave-block poll groups, its N = 6 4 workgroups per CU with
-    4-wave-block claims and poll groups, an 8-GPU rank's N = 7 the same with claims of 8."""
+    4-wave-block claims and 2-wave-block poll groups, an 8-GPU rank's N = 7 4 per CU with
+    claims of 8 and poll groups of 4."""
     # [1,2,3,4]/6 on a workerBits-3 rank (R = 32): 16^6 * 32 / 256 = 2^21 expected candidates
     d, = geometry([1, 2, 3, 4], 5, 3, 1, 1 << 24, 256, ntz=6)
     assert d.worker_blocks <= 2 * 256 and d.chunk_tail <= 2 and d.poll_wb == 1 and d.n_static > 0
@@ -193,8 +194,8 @@ def test_short_search_grids():
     d, = geometry([1, 2, 3, 4], 0, 0, 1, 1 << 20, 256, ntz=7)
     assert d.worker_blocks == 1280 and d.poll_wb == 8
     check(d, grid_cap(256))
-    d, = geometry([1, 2, 3, 4], 0, 0, 1, 1 << 20, 256, ntz=6)  # 2^24 expected: 4 per CU, claims of 4
-    assert d.worker_blocks == 1024 and d.poll_wb == 4 and d.chunk == 4
+    d, = geometry([1, 2, 3, 4], 0, 0, 1, 1 << 20, 256, ntz=6)  # 2^24 expected: 4 per CU, claims of 4, polls of 2
+    assert d.worker_blocks == 1024 and d.poll_wb == 2 and d.chunk == 4
     check(d, grid_cap(256))
     # an 8-GPU rank's [1,2,3,4]/7 (2^25 expected): the same mid tier
     d, = geometry([1, 2, 3, 4], 6, 3, 1, 1 << 24, 256, ntz=7)

@@ -242,10 +242,11 @@ int poll_node(dpow_ctx *c, SearchWait &sw) {
         // keeps the injected bound (ext_bound) that tells another rank's index from ours.
         // Our own hit, posted early (poll_early), is not a bound.
         sw.node_seen = nb;
-        if (nb == sw.own_posted) return 0;
-        std::lock_guard<std::mutex> g(c->bound_mu);
-        uint64_t cur = c->ext_bound.load(std::memory_order_relaxed);
-        if (nb < cur) c->ext_bound.store(nb, std::memory_order_release);
+        if (nb != sw.own_posted) {
+            std::lock_guard<std::mutex> g(c->bound_mu);
+            uint64_t cur = c->ext_bound.load(std::memory_order_relaxed);
+            if (nb < cur) c->ext_bound.store(nb, std::memory_order_release);
+        }
     }
     if (!sw.node_stop && __atomic_load_n(&n->stop, __ATOMIC_ACQUIRE) != 0u) {
         sw.node_stop = true;
@@ -725,13 +726,15 @@ void dpow_close(dpow_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    // Drained: no watcher of ours reads the node pages any more.  Leave the page registry
+    // before the stream is destroyed (dpow_node_release synchronizes every holder's stream).
+    c->node = c->d_node = nullptr;
+    pages_release_ctx(c);
     if (c->d_ctrl_alloc) (void)hipFree(c->d_ctrl_alloc);
     if (c->d_claims) (void)hipFree(c->d_claims);
     if (c->h_snap) (void)hipHostFree(c->h_snap);
     if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    c->node = c->d_node = nullptr;
-    pages_release_ctx(c);  // after the stream drained: no watcher of ours reads the pages any more
     delete c;
 }
 

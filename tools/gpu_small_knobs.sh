@@ -1,5 +1,5 @@
 # Short-search launch knobs on the BASELINE cases and over fresh nonces (tools/small_search_probe.py):
-#   gpurun --timeout 600 -- bash tools/gpu_r04_small2.sh <tag> bpc,min_chunk,poll_wb,cpw ...
+#   gpurun --timeout 600 -- bash tools/gpu_small_knobs.sh <tag> bpc,min_chunk,poll_wb,cpw ...
 set -o pipefail
 tag=$1; shift
 mkdir -p gpurun_out/$tag

@@ -542,7 +542,45 @@ def coordinator_configs():
             x.join(120)
         assert len(done) == 4
         out["config5_two_clients_total_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+    # Config 4's one nonce times one draw (which worker holds the first hit, and the share of the
+    # device its search got); over fresh nonces the mean follows the device's aggregate rate.
+    import random
+    rng = random.Random(20261017)
+    with Coordinator(8) as c:
+        ms = [timed(c, [rng.randrange(256) for _ in range(4)], 8) for _ in range(12)]
+    out["config4_12_fresh_nonces_mean_ms"] = round(sum(ms) / len(ms), 3)
+    out["shared_device_8_searches_ghs"] = shared_device_rate(8)
     return out
+
+
+def shared_device_rate(w, span=26):
+    """Aggregate GH/s of w searches at once on this GPU (the coordinator mirror's logical
+    workers: worker i of workerBits log2(w), k in [2^24, 2^24 + 2^span), N = 32, no hit), from
+    their common start to the last one's end (plan.h grid_share, cap_shared_launch)."""
+    import threading
+    bits = w.bit_length() - 1
+    miners = [distpow.Miner(0) for _ in range(w)]  # world 1: this rank's GPU
+    try:
+        for m in miners:
+            m.search(NONCE, 32, 0, bits, 1 << 24, (1 << 24) + (1 << 16))
+        go = threading.Barrier(w + 1)
+        ends = [0.0] * w
+
+        def run(i):
+            go.wait()
+            assert miners[i].search(NONCE, 32, i, bits, 1 << 24, (1 << 24) + (1 << span)).status == distpow.EXHAUSTED
+            ends[i] = time.perf_counter()
+        th = [threading.Thread(target=run, args=(i,)) for i in range(w)]
+        for x in th:
+            x.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for x in th:
+            x.join(60)
+        return round(w * ((1 << span) << (8 - bits)) / (max(ends) - t0) / 1e9, 1)
+    finally:
+        for m in miners:
+            m.close()
 
 
 def cancel_latency(miner, reps=3, run_s=0.05):

@@ -108,7 +108,7 @@ constexpr int64_t kNoDeadline = INT64_MAX;
 // the fixed cost below the measured one), so a window without a hit runs its
 // launches back to back.
 constexpr int64_t kQueueLeadNs = 60000;
-constexpr double kEstRate = 2.3e11;  // candidates/s of one device (bench: 217-218 on the one-block layouts)
+// (kEstRate: plan.h)
 constexpr int64_t kEstFixedNs = 8000;
 
 // Searches in flight per device in this process.  Several logical workers may
@@ -117,6 +117,7 @@ constexpr int64_t kEstFixedNs = 8000;
 // search then sizes its persistent grids to its share of the device, so the
 // worker holding the answer is not starved by grids that fill every CU slot.
 constexpr int kMaxDevices = 64;
+
 std::atomic<int> g_active[kMaxDevices];
 
 struct ActiveSearch {
@@ -205,7 +206,8 @@ struct dpow_ctx {
     dpow_node_slot *d_node = nullptr;  // its device alias (the watcher polls it)
     // A/B overrides of the launch policy (dpow_diag.h): DPOW_DIAG_POLL_WB (wave-blocks per poll
     // group), DPOW_DIAG_BPC (worker workgroups per CU), DPOW_DIAG_MIN_CHUNK (minimum wave-blocks
-    // per claim, a power of two), DPOW_DIAG_CPW (big claims per wave); 0 = the policy.
+    // per claim, a power of two), DPOW_DIAG_CPW (big claims per wave), DPOW_DIAG_SHARE_LAUNCH_US
+    // (launch length on a shared device), DPOW_DIAG_SHARE_MAX (grid share cap); 0 = the policy.
     LaunchKnobs knobs;
     int64_t diag_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // the last search's host timeline (dpow_diag_search_times)
 };
@@ -525,10 +527,13 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         if ((rc = retire_slot(c, slot)) < 0) return rc;  // the slot's previous user
         if (!md5_queued) c->diag_t[6] = now_ns() - sw.t0;
         Launch &L = pl.L;
-        // This search's share of the device's resident workgroups (1 / searches in flight on it).
-        const uint64_t share = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
+        // This search's share of the device's resident workgroups (searches sharing the device:
+        // plan.h grid_share, cap_shared_launch).
+        const uint64_t active = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
+        const uint64_t share = grid_share(active, c->knobs);
+        cap_shared_launch(planner, pl, active, c->knobs);
         uint64_t worker_blocks = 0;
-        rc = size_search_launch(pl, ntz, c->cus, share, c->knobs, &worker_blocks);
+        rc = size_search_launch(pl, ntz, c->cus, share, c->knobs, &worker_blocks, active);
         if (rc < 0) return set_error(rc, "dpow_search: launch grid leaves a claim counter without waves");
         done_target += (uint32_t)worker_blocks;  // retirement is counted per workgroup
         L.claim = c->d_claims + (li % kClaimRing) * kClaimSlot;
@@ -558,7 +563,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         ++launched;
         const int64_t t = now_ns();
         busy_until = std::max(busy_until, t) + kEstFixedNs +
-                     (int64_t)((double)slot.candidates * (double)share / kEstRate * 1e9);
+                     (int64_t)((double)slot.candidates * (double)active / kEstRate * 1e9);
         have = planner.next(pl);
     }
     while (status == DPOW_EXHAUSTED && consumed < launched) {  // the window is queued: drain in order
@@ -678,6 +683,8 @@ int dpow_open(int device, dpow_ctx **out) {
     if (const char *pw = getenv("DPOW_DIAG_POLL_WB")) c->knobs.poll_wb = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_BPC")) c->knobs.bpc = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_CPW")) c->knobs.cpw = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_SHARE_LAUNCH_US")) c->knobs.share_launch_us = (uint32_t)std::max(0, atoi(pw));
+    if (const char *pw = getenv("DPOW_DIAG_SHARE_MAX")) c->knobs.share_max = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_MIN_CHUNK")) {
         const uint32_t v = (uint32_t)std::max(0, atoi(pw));
         if (v && !(v & (v - 1))) c->knobs.min_chunk = v;
@@ -995,10 +1002,13 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t n
     if (rc < 0) return set_error(rc, "dpow_diag_launch_geometry: bad arguments");
     PlannedLaunch pl;
     size_t n = 0;
+    const LaunchKnobs policy{};
     while (planner.next(pl)) {
         if (pl.k0) continue;  // k = 0: the search's k = 0 kernel, not an md5 launch
+        // share = searches in flight on the device, as dpow_search sees them (g_active)
+        cap_shared_launch(planner, pl, share, policy);
         uint64_t wblocks = 0;
-        const int r = size_search_launch(pl, ntz, cus, share, LaunchKnobs{}, &wblocks);
+        const int r = size_search_launch(pl, ntz, cus, grid_share(share, policy), policy, &wblocks, share);
         if (r < 0) return set_error(r, "dpow_diag_launch_geometry: launch grid leaves a claim counter without waves");
         if (out && n < max_launches) {
             dpow_diag_launch &d = out[n];

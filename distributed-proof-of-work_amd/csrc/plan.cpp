@@ -127,6 +127,9 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
         const uint64_t we = (k / w2 + 1) * w2;
         if (we < ke) ke = we;
     }
+    const uint64_t cap_end = cap_k_ && k_end_ - k > cap_k_ ? k + cap_k_ : k_end_;
+    cap_k_ = 0;
+    if (cap_end < ke) ke = cap_end;
     const uint32_t L = chunk_len_of(k);
     const uint32_t nblk = nblk_of(L);
     pl.k0 = DPOW_START_K0 && k == 0;
@@ -135,7 +138,8 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     if (!pl.k0 && k >= 1 && lseg_template(k)) {
         // Merge the following chunk lengths (up to 3) with the same block count.
         uint64_t e = ke;
-        while (e < k_end_ && e < lspan_end_ && nblk_of(chunk_len_of(e)) == nblk) {
+        while (e < k_end_ && e < lspan_end_ && nblk_of(chunk_len_of(e)) == nblk &&
+               (segment_end(e) < k_end_ ? segment_end(e) : k_end_) <= cap_end) {  // whole segments only
             e = segment_end(e) < k_end_ ? segment_end(e) : k_end_;
             L_last = chunk_len_of(e - 1);
         }
@@ -327,10 +331,12 @@ uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits) {
 }
 
 int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t share, const LaunchKnobs &knobs,
-                       uint64_t *worker_blocks) {
+                       uint64_t *worker_blocks, uint64_t active) {
     Launch &L = pl.L;
-    const uint64_t bpc = knobs.bpc ? knobs.bpc : launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits);
-    const uint64_t max_blocks = std::max<uint64_t>(cus * bpc / std::max<uint64_t>(share, 1), kClaimCounters);
+    share = std::max<uint64_t>(share, 1);
+    active = std::max<uint64_t>(active, share);
+    const uint64_t bpc = knobs.bpc ? knobs.bpc : launch_blocks_per_cu(L.i_end - L.i_begin, ntz, L.rbits, active);
+    const uint64_t max_blocks = std::max<uint64_t>(cus * bpc / share, kClaimCounters);
     const int rc = size_launch(pl, max_blocks, expected_first_hit(ntz, L.rbits), worker_blocks,
                                knobs.min_chunk ? knobs.min_chunk : launch_min_chunk(ntz, L.rbits),
                                knobs.cpw ? knobs.cpw : launch_claims_per_wave(ntz, L.rbits));
@@ -344,17 +350,34 @@ int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t s
     return 0;
 }
 
-uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits) {
+uint64_t grid_share(uint64_t active, const LaunchKnobs &knobs) {
+    const uint64_t cap = knobs.share_max ? knobs.share_max : kShareMax;
+    return std::max<uint64_t>(1, std::min(active, cap));
+}
+
+bool cap_shared_launch(WindowPlanner &planner, PlannedLaunch &pl, uint64_t active, const LaunchKnobs &knobs) {
+    if (active <= 1 || pl.k0) return false;
+    const double ns = knobs.share_launch_us ? knobs.share_launch_us * 1e3 : (double)kShareLaunchNs;
+    const uint64_t cap_k = std::max<uint64_t>(1, (uint64_t)(kEstRate / (double)active * ns * 1e-9) >> pl.L.rbits);
+    if (pl.info.k_end - pl.info.k_begin <= cap_k) return false;
+    planner.restart(pl.info.k_begin, cap_k);
+    planner.next(pl);
+    return true;
+}
+
+uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits, uint64_t share) {
 #if DPOW_SMALL_GRIDS
-    // Candidates of this partition expected before its first hit: 16^N R / 256.
-    const uint64_t expect = expected_first_hit(ntz, rbits);
-    const uint64_t eff = candidates < expect ? candidates : expect;
+    // Candidates of this partition expected before its first hit: 16^N R / 256, and the
+    // launch's, in device time (times the searches sharing the device; saturating).
+    const auto dev = [share](uint64_t v) { return share > 1 && v > ~0ull / share ? ~0ull : v * (share ? share : 1); };
+    const uint64_t expect = dev(expected_first_hit(ntz, rbits));
+    const uint64_t eff = dev(candidates) < expect ? dev(candidates) : expect;
     if (eff <= kTinyExpect) return kMaxBlocksPerCu < 2 ? kMaxBlocksPerCu : 2;
     if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
     if (eff <= kMidExpect) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
     if (kFiveExpect && expect <= kFiveExpect) return kMaxBlocksPerCu < 5 ? kMaxBlocksPerCu : 5;
 #else
-    (void)candidates, (void)ntz, (void)rbits;
+    (void)candidates, (void)ntz, (void)rbits, (void)share;
 #endif
     return kMaxBlocksPerCu;
 }

@@ -44,6 +44,13 @@ class WindowPlanner {
     int init(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte, uint32_t worker_bits,
              uint64_t k_begin, uint64_t k_end);
     bool next(PlannedLaunch &out);  // false when the window is covered
+    // Re-plan from k (the start of the launch next() last returned) with that launch at
+    // most max_k k long (no chunk-length merging past it): dpow_search's launches while
+    // the device is shared.
+    void restart(uint64_t k, uint64_t max_k) {
+        k_ = k;
+        cap_k_ = max_k;
+    }
 
    private:
     uint32_t nblk_of(uint32_t chunk_len) const;
@@ -53,6 +60,7 @@ class WindowPlanner {
     size_t nonce_len_ = 0, blk_v_ = 0;
     uint32_t p_ = 0, ntz_ = 0, rbits_ = 0, base_tb_ = 0;
     uint64_t k_ = 0, k_end_ = 0;
+    uint64_t cap_k_ = 0;  // one-shot length cap of the next launch (restart), 0: none
     uint64_t lspan_end_ = 0;  // launches below this k use the chunk-length-0 template and may span
     uint32_t iv_[4] = {0, 0, 0, 0};
 };
@@ -193,7 +201,11 @@ uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits);
 #define DPOW_SMALL_GRIDS 1  // fewer workgroups per CU for short launches (A/B switch)
 #endif
 constexpr uint64_t kMaxBlocksPerCu = DPOW_BLOCKS_PER_CU;
-uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits);
+// share: searches in flight on the device (dpow_api.cpp g_active).  Such a search runs at
+// 1/share of the device, so the tiers judge its launch by device time: candidates and the
+// expected first hit times share.  BASELINE config 4 (8 logical workers on one GPU, N = 8,
+// 2^29 expected each) keeps the full grid.
+uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits, uint64_t share = 1);
 
 // The whole sizing of one dpow_search launch, shared by dpow_search and the geometry
 // diagnostic (dpow_diag_launch_geometry), so the diagnostic checks the grids searches run:
@@ -204,8 +216,38 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits)
 constexpr double kFairRate = 2.05e11;  // candidates/s of a device at 4-6 workgroups per CU (one block)
 struct LaunchKnobs {
     uint32_t bpc = 0, min_chunk = 0, cpw = 0, poll_wb = 0;
+    uint32_t share_launch_us = 0;  // launch length on a shared device (kShareLaunchNs)
+    uint32_t share_max = 0;        // grid share cap (kShareMax)
 };
+// share: the grid is 1/share of the device's; active (>= share): the searches in flight on the
+// device, which set the launch's device time (launch_blocks_per_cu).
 int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t share, const LaunchKnobs &knobs,
-                       uint64_t *worker_blocks);
+                       uint64_t *worker_blocks, uint64_t active = 1);
+
+// Searches sharing a device (dpow_api.cpp g_active): the coordinator mirror's logical workers
+// on one GPU (BASELINE configs 3-5: 4 or 8 workers per GPU in the 1-GPU bench).
+//  - A grid is sized once per launch, so while the device is shared a launch lasts about
+//    kShareLaunchNs at 1/active of the device's rate (cap_shared_launch): grids follow searches
+//    that start or end beside it.  (One launch per window kept a grid sized for a crowd after
+//    the crowd was gone: the last of 4 searches ran 47 ms on 1 workgroup per CU.)
+//  - A grid is 1/min(active, kShareMax) of the device (grid_share).  The HIP runtime maps a
+//    process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and the kernels of streams
+//    sharing a queue run one after the other: grids of 1/active left the device part-idle.
+//    Each search's grid at 1/2 keeps it full across launch boundaries (8 concurrent searches of
+//    2^31 candidates: 163-168 GH/s at 1/8, 197 at 1/4, 210-215 at 1/2; BASELINE config 4 over
+//    16 fresh nonces 29.8 -> 20.1 ms mean, profiles/r04_share/).
+#ifndef DPOW_SHARE_MAX
+#define DPOW_SHARE_MAX 2
+#endif
+#ifndef DPOW_SHARE_LAUNCH_US
+#define DPOW_SHARE_LAUNCH_US 2000
+#endif
+constexpr uint64_t kShareMax = DPOW_SHARE_MAX;
+constexpr int64_t kShareLaunchNs = (int64_t)DPOW_SHARE_LAUNCH_US * 1000;
+constexpr double kEstRate = 2.3e11;  // candidates/s of one device (bench: 217-218 on the one-block layouts)
+uint64_t grid_share(uint64_t active, const LaunchKnobs &knobs);
+// Re-plans pl (the launch planner.next() last returned) to at most kShareLaunchNs of hashing
+// when active > 1; returns whether it did.
+bool cap_shared_launch(WindowPlanner &planner, PlannedLaunch &pl, uint64_t active, const LaunchKnobs &knobs);
 
 }  // namespace dpow

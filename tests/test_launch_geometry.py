@@ -41,17 +41,22 @@ def geometry(nonce, wb, wbits, k0, k1, cus, share=1, ntz=32):
                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(DiagLaunch),
                    ctypes.c_size_t]
     n = bytes(nonce)
-    arr = (DiagLaunch * 16)()
-    cnt = fn(n, len(n), ntz, wb, wbits, k0, k1, cus, share, arr, 16)
+    cnt = fn(n, len(n), ntz, wb, wbits, k0, k1, cus, share, None, 0)
     assert cnt >= 0, distpow._lib.last_error()
-    assert cnt <= 16
+    arr = (DiagLaunch * max(cnt, 1))()
+    assert fn(n, len(n), ntz, wb, wbits, k0, k1, cus, share, arr, cnt) == cnt
     return list(arr[:cnt])
 
 
+SHARE_MAX = 2  # plan.h kShareMax: a grid is at most 1/2 of the device's however many searches share it
+EST_RATE = 2.3e11  # plan.h kEstRate
+SHARE_LAUNCH_NS = 2_000_000  # plan.h kShareLaunchNs
+
+
 def grid_cap(cus, share=1):
-    """The most worker workgroups a launch can get: the full 6-per-CU grid's share, at least
-    one per claim counter."""
-    return max(cus * 6 // share, CLAIM_COUNTERS)
+    """The most worker workgroups a launch can get: the full 6-per-CU grid's share (searches in
+    flight, capped at SHARE_MAX), at least one per claim counter."""
+    return max(cus * 6 // min(share, SHARE_MAX), CLAIM_COUNTERS)
 
 
 def check(d, max_blocks):
@@ -131,7 +136,10 @@ def test_large_and_small_windows():
         ntz = rnd.choice([32, 3, 5, 6, 7, 8, 9])
         for cus, share in ((1, 1), (16, 1), (256, 8), (256, 2), (256, 1)):  # shares, the 2 / 3 / 4 / 6-per-CU grids
             for nonce in ([1, 2, 3, 4], [1, 2]):  # SH 0; SH 2 (word W0+2 splits at L = 6)
-                for d in geometry(nonce, wb, wbits, k0, k1, cus, share, ntz):
+                ds = geometry(nonce, wb, wbits, k0, k1, cus, share, ntz)
+                assert (not ds and k1 == 1) or ds[-1].k_end == k1
+                assert all(a.k_end == b.k_begin for a, b in zip(ds, ds[1:]))
+                for d in ds if len(ds) <= 64 else ds[:32] + ds[-32:]:  # a shared device's ~2 ms launches
                     check(d, grid_cap(cus, share))
 
 
@@ -160,6 +168,10 @@ def test_chunk_length_spanning_launches(ntz):
         le = lspan_end(ntz, 8 - wbits)
         assert ds[0].k_begin == max(k0, 1) and ds[-1].k_end == k1
         assert all(a.k_end == b.k_begin for a, b in zip(ds, ds[1:]))
+        if share > 1:  # a shared device: launches of at most ~2 ms at 1/share of the rate
+            for d in ds:
+                check(d, grid_cap(cus, share))
+            continue
         if k1 <= le or max(k0, 1) >= le:
             assert len(ds) == 1, (len(nonce), k0, k1, [(d.k_begin, d.k_end) for d in ds])
         else:
@@ -223,3 +235,36 @@ def test_grid_policy_for_short_launches():
     for n in range(0, 40, 3):  # never more than the full grid, monotone in the launch size
         seq = [f(1 << n, z, 0) for z in range(0, 34)]
         assert all(2 <= b <= 6 for b in seq) and seq == sorted(seq)
+
+
+def test_shared_device_launches():
+    """Searches sharing a device (dpow_search's g_active; plan.h grid_share, cap_shared_launch):
+    launches of about kShareLaunchNs at 1/active of the device's rate, tiling the window, each
+    grid 1/min(active, 2) of the device's, and the workgroups per CU chosen on the launch's
+    device time (BASELINE config 4: 8 workers on one GPU at N = 8, 2^29 candidates expected
+    each, keep the full 6-per-CU grid; alone, an 8-GPU rank's N = 8 gets 5)."""
+    nonce = [1, 2, 3, 4]
+    for active in (2, 4, 8):
+        for wbits, ntz, k0, k1 in ((3, 8, 1 << 16, 1 << 24), (2, 7, 1 << 16, 1 << 24), (0, 32, 1 << 24, 1 << 30),
+                                    (3, 32, 1 << 24, (1 << 24) + (1 << 27))):
+            ds = geometry(nonce, 5 % (1 << wbits), wbits, k0, k1, 256, active, ntz)
+            rbits = 8 - wbits
+            cap_k = max(1, int(EST_RATE / active * SHARE_LAUNCH_NS * 1e-9) >> rbits)
+            assert ds[0].k_begin == k0 and ds[-1].k_end == k1
+            assert all(a.k_end == b.k_begin for a, b in zip(ds, ds[1:]))
+            assert all(d.k_end - d.k_begin <= cap_k for d in ds)
+            assert len(ds) == -(-(k1 - k0) // cap_k) or k0 < (1 << 24) < k1
+            for d in ds:
+                check(d, grid_cap(256, active))
+            if ntz == 32 or (wbits, ntz) == (3, 8):  # 2^29 x active > 2^31 (plan.h kFiveExpect): the full grid
+                bpc = 6 if ntz == 32 or active > 4 else 5
+                assert all(d.worker_blocks == 256 * bpc // min(active, SHARE_MAX) for d in ds), \
+                    [d.worker_blocks for d in ds]
+    # alone: one launch per segment, the tiers of the search's own expected first hit
+    d, = geometry(nonce, 5, 3, 1 << 16, 1 << 24, 256, 1, 8)
+    assert d.worker_blocks == 256 * 5
+    d, = geometry(nonce, 5, 3, 1 << 16, 1 << 24, 256, 8, 32)[:1]
+    assert d.worker_blocks == 256 * 6 // SHARE_MAX
+    # the tiers judge device time: 4 workers at N = 7 (2^26 expected each, 2^28 of device time)
+    assert {d.worker_blocks for d in geometry(nonce, 1, 2, 1 << 16, 1 << 24, 256, 4, 7)} == {256 * 5 // 2}
+    assert {d.worker_blocks for d in geometry(nonce, 1, 2, 1 << 16, 1 << 24, 256, 1, 7)} == {256 * 4}

@@ -472,6 +472,35 @@ def test_deep_hits_golden(miner, golden):
         assert _hexz(e["nonce"], r.secret) == e["md5"] and e["md5"].endswith("0" * e["ntz"])
 
 
+def test_concurrent_deep_hits_in_shared_launches(golden):
+    """The four config-5 fresh nonces at N = 9 mined at once on one GPU: while the device is
+    shared, dpow_search cuts each window into ~2 ms launches and re-sizes every grid
+    (plan.h grid_share, cap_shared_launch), so each hit (4.5e10-1.1e11 candidates in) lies
+    behind hundreds of launch boundaries.  Every answer is still the golden."""
+    deep = [e for e in golden["deep_hits"] if e["case"].startswith("config5-fresh")]
+    assert len(deep) == 4
+    miners = [distpow.Miner(0) for _ in deep]
+    out = {}
+    try:
+        def run(i, e):
+            miners[i].reset_stats()
+            out[i] = (miners[i].mine(e["nonce"], e["ntz"]), miners[i].stats().launches)
+        ths = [threading.Thread(target=run, args=(i, e)) for i, e in enumerate(deep)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=90)
+        assert not any(t.is_alive() for t in ths)
+        for i, e in enumerate(deep):
+            r, launches = out[i]
+            assert r.status == FOUND and (r.global_idx, list(r.secret)) == (e["global_idx"], e["secret"]), (e, r)
+        # the shortest search ran beside the three others throughout: many short launches
+        assert min(n for _, n in out.values()) >= 20, {i: n for i, (_, n) in out.items()}
+    finally:
+        for m in miners:
+            m.close()
+
+
 def test_n10_min_over_8_partitions(miner, golden):
     """N = 10 on [1,2,3,4] (1.1e12 candidates expected; about 5 s per pass): the minimum of
     the 8 workerBits = 3 partitions' first hits is the workerBits = 0 golden, and the

@@ -114,10 +114,10 @@ constexpr int64_t kEstFixedNs = 8000;
 // Searches in flight per device in this process.  Several logical workers may
 // share one GPU (the coordinator mirror places W workers round-robin on the
 // node's devices; BASELINE config 4 runs 8 on one in the 1-GPU bench): each
-// search then sizes its persistent grids to its share of the device, so the
-// worker holding the answer is not starved by grids that fill every CU slot.
+// search then sizes its persistent grids to its share of the device and keeps its
+// launches short (plan.h grid_share, cap_shared_launch), so the device stays full and
+// every search's grid follows the others that start or end beside it.
 constexpr int kMaxDevices = 64;
-
 std::atomic<int> g_active[kMaxDevices];
 
 struct ActiveSearch {

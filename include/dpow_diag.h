@@ -51,10 +51,11 @@ int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, u
                          uint32_t iv_d, uint32_t state_d);
 
 /* Claim geometry dpow_search gives each launch of a window (host logic, no GPU), sized by
- * the same function dpow_search uses (plan.cpp size_search_launch): the device share
- * (cus x the ntz- and size-dependent workgroups per CU / share, at least one per claim
- * counter), the expected first hit at ntz, the minimum chunk, the claims per wave and the
- * poll group.  `share` is the number of searches in flight on the device (1 alone).  One
+ * the same functions dpow_search uses (plan.cpp size_search_launch, grid_share,
+ * cap_shared_launch): the device share (cus x the ntz- and size-dependent workgroups per CU
+ * / min(share, 2), at least one per claim counter), the expected first hit at ntz, the
+ * minimum chunk, the claims per wave and the poll group.  `share` is the number of searches
+ * in flight on the device (1 alone); above 1 the window is cut into ~2 ms launches.  One
  * entry per launch; returns the number of launches (only the first max_launches are
  * written), or < 0 when a launch would leave a claim counter without waves.
  * (ABI 3: ntz, cus and share replace round 3's max_blocks, which sized every launch as an
@@ -78,20 +79,23 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t n
                               uint32_t share, dpow_diag_launch *out, size_t max_launches);
 
 /* Worker workgroups per CU dpow_search gives a launch of `candidates` local indices
- * at (ntz, worker_bits), before dividing by the searches sharing the device: 6 (the
- * full persistent grid) unless the launch is short -- at most 2^24 candidates, or a
- * first hit expected within that many (16^ntz R / 256) -- then 4, or 3 at 2^22. */
+ * at (ntz, worker_bits) on a device it has alone (plan.cpp launch_blocks_per_cu): 6 (the
+ * full persistent grid) unless the launch is short or a first hit is expected early
+ * (16^ntz R / 256 candidates): 2 up to 2^21, 3 up to 2^22, 4 up to 2^26 candidates, and 5
+ * while the hit is expected within 2^31. */
 uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t worker_bits);
 
 /* Host timeline of the context's last dpow_search call, ns from its start (-1: did not
  * happen): [0] the k = 0 kernel queued, [1] the first md5 launch queued, [2] the first
  * completion record seen, [3] the search done (before the host MD5 re-verification),
  * [4] the first launch planned, [5] the k = 0 kernel's record slot retired, [6] the
- * first md5 launch's record slot retired, [7] unused.
+ * first md5 launch's record slot retired, [7] the search's own hit posted to its node slot
+ * by the early Found fan-out.
  * Environment overrides read at dpow_open (A/B runs only): DPOW_DIAG_POLL_WB (wave-blocks
  * per poll group), DPOW_DIAG_BPC (worker workgroups per CU), DPOW_DIAG_MIN_CHUNK (minimum
  * wave-blocks per claim, a power of two), DPOW_DIAG_CPW (big claims per wave: the chunk
- * sizing).  Returns 0, or < 0 on error. */
+ * sizing), DPOW_DIAG_SHARE_LAUNCH_US (launch length while the device is shared),
+ * DPOW_DIAG_SHARE_MAX (grid share cap).  Returns 0, or < 0 on error. */
 int dpow_diag_search_times(struct dpow_ctx *ctx, int64_t out[8]);
 
 /* Node emulation on one GPU (tools/node_probe.py): post global_idx to a node slot

@@ -101,12 +101,14 @@ def main():
     device = 0 if args.same_device else local_rank
     torch.cuda.set_device(device)
     tick_group = None
+    host_group = None  # world > 1 over RCCL: a gloo group; else the default group
     dist_on = world > 1 or not args.no_dist
     if world > 1:
         if args.backend == "nccl":  # RCCL over xGMI
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
             if not NODE_SYNC:  # node_mine_async's ticks: a host (gloo) group, off the busy GPUs
                 tick_group = dist.new_group(backend="gloo")
+            host_group = dist.new_group(backend="gloo")  # host-only barriers (no GPU kernel waits)
         else:
             dist.init_process_group("gloo")
     elif dist_on:
@@ -255,6 +257,15 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_tts:
         extra["coordinator"] = coordinator_configs()
+    if world > 1 and not args.no_tts:
+        # BASELINE configs 3-5 in their node shape: rank 0's process runs the coordinator mirror
+        # with logical worker i on GPU i % world (coordinator.go:139-298 over W machines), while
+        # the other ranks wait on a host barrier with their GPUs idle.
+        dist.barrier(group=host_group)
+        if rank == 0:
+            extra["coordinator_node"] = coordinator_configs(devices=[0] * world if args.same_device
+                                                            else list(range(world)))
+        dist.barrier(group=host_group)
 
     probe = {}
     if rank == 0 and not args.no_probe:
@@ -507,10 +518,11 @@ def collective_probe(miner, rank, world, dev, board, backend, reps=200):
             "node_mine": tts}
 
 
-def coordinator_configs():
+def coordinator_configs(devices=(0,)):
     """BASELINE configs 3-5 end to end through the coordinator mirror (coordinator.go:139-320)
-    over native workers (worker.go:169-232), all logical workers on this rank's GPU: wall ms
-    per client request, first-arrived answers as the reference gives them, each verified."""
+    over native workers (worker.go:169-232), logical worker i on devices[i % len(devices)] (one
+    GPU: all of them on this rank's): wall ms per client request, first-arrived answers as the
+    reference gives them, each verified."""
     import threading
     from distpow.coordinator import Coordinator
 
@@ -520,13 +532,14 @@ def coordinator_configs():
         assert distpow.verify(nonce, s, n)
         return round((time.perf_counter() - t) * 1e3, 3)
 
-    out = {}
-    with Coordinator(4) as c:  # config 3: 4 workers (workerBits = 2), N = 7, cold then warm cache
+    devices = list(devices)
+    out = {"devices": devices} if len(devices) > 1 else {}
+    with Coordinator(4, devices) as c:  # config 3: 4 workers (workerBits = 2), N = 7, cold then warm cache
         out["config3_4workers_n7_cold_ms"] = timed(c, [1, 2, 3, 4], 7)
         out["config3_4workers_n7_warm_ms"] = timed(c, [1, 2, 3, 4], 7)
-    with Coordinator(8) as c:  # config 4: 8 workers (workerBits = 3), N = 8
+    with Coordinator(8, devices) as c:  # config 4: 8 workers (workerBits = 3), N = 8
         out["config4_8workers_n8_ms"] = timed(c, [1, 2, 3, 4], 8)
-    with Coordinator(4) as c:  # config 5: two concurrent clients (cmd/client/main.go:40-51)
+    with Coordinator(4, devices) as c:  # config 5: two concurrent clients (cmd/client/main.go:40-51)
         reqs = [([1, 2, 3, 4], 7), ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5), ([2, 2, 2, 2], 7)]
         done = {}
 
@@ -546,20 +559,21 @@ def coordinator_configs():
     # device its search got); over fresh nonces the mean follows the device's aggregate rate.
     import random
     rng = random.Random(20261017)
-    with Coordinator(8) as c:
+    with Coordinator(8, devices) as c:
         ms = [timed(c, [rng.randrange(256) for _ in range(4)], 8) for _ in range(12)]
     out["config4_12_fresh_nonces_mean_ms"] = round(sum(ms) / len(ms), 3)
-    out["shared_device_8_searches_ghs"] = shared_device_rate(8)
+    if len(devices) == 1:
+        out["shared_device_8_searches_ghs"] = shared_device_rate(8, devices[0])
     return out
 
 
-def shared_device_rate(w, span=26):
+def shared_device_rate(w, device=0, span=26):
     """Aggregate GH/s of w searches at once on this GPU (the coordinator mirror's logical
     workers: worker i of workerBits log2(w), k in [2^24, 2^24 + 2^span), N = 32, no hit), from
     their common start to the last one's end (plan.h grid_share, cap_shared_launch)."""
     import threading
     bits = w.bit_length() - 1
-    miners = [distpow.Miner(0) for _ in range(w)]  # world 1: this rank's GPU
+    miners = [distpow.Miner(device) for _ in range(w)]
     try:
         for m in miners:
             m.search(NONCE, 32, 0, bits, 1 << 24, (1 << 24) + (1 << 16))

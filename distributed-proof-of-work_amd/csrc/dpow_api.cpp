@@ -49,6 +49,24 @@ int hip_fail(hipError_t e, const char *what) {
     return set_error(DPOW_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// The calling thread's current device (HIP per-thread state) for the duration of an
+// entry point, restored on return: a host thread that drives several GPUs -- one rank's
+// coordinator mirror with a worker per GPU, torch's current device -- keeps its own.
+struct DeviceScope {
+    int prev = -1;
+    hipError_t e = hipSuccess;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) e = hipSetDevice(dev);
+        if (prev == dev) prev = -1;  // nothing to restore
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 // Internal status of consume(): the window holds nothing below a bound injected
 // by dpow_search_bound (reported as DPOW_EXHAUSTED).
 constexpr int DPOW_BOUNDED = 3;
@@ -341,7 +359,8 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     WindowPlanner planner;
     int rc = planner.init(nonce, nonce_len, ntz, worker_byte, worker_bits, k_begin, k_end);
     if (rc < 0) return set_error(rc, "dpow_search: planning failed");
-    DPOW_HIP(hipSetDevice(c->device));
+    const DeviceScope on_device(c->device);
+    if (on_device.e != hipSuccess) return hip_fail(on_device.e, "hipSetDevice");
     if (c->device >= kMaxDevices) return set_error(DPOW_EINVAL, "dpow_search: device ordinal too large");
     const ActiveSearch active(c->device);
     SearchWait sw;
@@ -670,7 +689,8 @@ int dpow_open(int device, dpow_ctx **out) {
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n == 0) return set_error(DPOW_EHIP, "dpow_open: no HIP device visible");
     if (device < 0 || device >= n) return set_error(DPOW_EINVAL, "dpow_open: bad device ordinal");
-    DPOW_HIP(hipSetDevice(device));
+    const DeviceScope on_device(device);
+    if (on_device.e != hipSuccess) return hip_fail(on_device.e, "hipSetDevice");
     dpow_ctx *c = new (std::nothrow) dpow_ctx();
     if (!c) return set_error(DPOW_ENOMEM, "dpow_open: out of memory");
     c->device = device;
@@ -731,7 +751,7 @@ int dpow_open(int device, dpow_ctx **out) {
 
 void dpow_close(dpow_ctx *c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    const DeviceScope on_device(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     // Drained: no watcher of ours reads the node pages any more.  Leave the page registry
     // before the stream is destroyed (dpow_node_release synchronizes every holder's stream).
@@ -783,7 +803,8 @@ int dpow_node_attach(dpow_ctx *c, dpow_node_slot *slot) {
     }
     if (((uintptr_t)slot & 7u) != 0u) return set_error(DPOW_EINVAL, "dpow_node_attach: slot not 8-byte aligned");
     // Map the slot's host page(s) for the watcher (fine-grained: hipHostRegister's default).
-    DPOW_HIP(hipSetDevice(c->device));
+    const DeviceScope on_device(c->device);
+    if (on_device.e != hipSuccess) return hip_fail(on_device.e, "hipSetDevice");
     const uintptr_t pg = 4096;
     {
         std::lock_guard<std::mutex> g(g_page_mu);
@@ -816,7 +837,7 @@ int dpow_node_release(void *mem, size_t len) {
         if (p < lo || p >= hi) continue;
         // launches a holder left queued behind its last search may still read the page
         for (dpow_ctx *h : g_pages[i].holders) {
-            (void)hipSetDevice(h->device);
+            const DeviceScope on_device(h->device);
             const hipError_t e = hipStreamSynchronize(h->stream);
             if (e != hipSuccess) return hip_fail(e, "dpow_node_release: hipStreamSynchronize");
         }

@@ -11,7 +11,9 @@
  * Ownership: the caller owns every host buffer passed in or out; the library
  * owns all device memory and the pinned cancel flag of a context.
  * Threading: one search in flight per context (the caller serialises); the
- * cancel flag may be written from any thread while a search runs.
+ * cancel flag may be written from any thread while a search runs.  An entry point
+ * that works on a context's GPU makes it the calling thread's current HIP device
+ * for the call and restores the caller's device on return.
  * Errors are returned as negative codes; nothing longjmps, throws or aborts.
  */
 #ifndef DPOW_H

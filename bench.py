@@ -263,8 +263,13 @@ def main():
         # the other ranks wait on a host barrier with their GPUs idle.
         dist.barrier(group=host_group)
         if rank == 0:
-            extra["coordinator_node"] = coordinator_configs(devices=[0] * world if args.same_device
-                                                            else list(range(world)))
+            ndev = max(1, torch.cuda.device_count())  # the GPUs this process sees
+            try:
+                extra["coordinator_node"] = coordinator_configs(
+                    devices=[0] * world if args.same_device else [i % ndev for i in range(world)])
+            except Exception as e:  # reported, not fatal: the sweep line above is the benchmark
+                log(f"rank 0: coordinator configs in the node shape failed: {e!r}")
+                extra["coordinator_node"] = {"error": repr(e)}
         dist.barrier(group=host_group)
 
     probe = {}

@@ -501,6 +501,57 @@ def test_concurrent_deep_hits_in_shared_launches(golden):
             m.close()
 
 
+def test_shared_capped_windows_vs_oracle(oracle, monkeypatch):
+    """Searches sharing the GPU cut their windows into short launches (plan.h
+    cap_shared_launch), each re-planned from where the last ended and re-sized to the searches
+    in flight.  With the launch length forced down to 2 us (DPOW_DIAG_SHARE_LAUNCH_US, read at
+    dpow_open), four concurrent searches over oracle-sized windows -- across the chunk-length
+    boundaries k = 256, 65536 and 2^24, every nonce-length family, hits anywhere in the window
+    or none -- run as 2-15 launches each, and every answer is the oracle's."""
+    rnd = random.Random(2026)
+    cases = []
+    for _ in range(16):
+        nonce = [rnd.randrange(256) for _ in range(rnd.choice([0, 3, 4, 4, 7, 50, 53, 55, 56, 59, 60, 63, 64]))]
+        wbits = rnd.choice([0, 0, 1, 2, 3, 5])
+        wb = rnd.randrange(1 << wbits) if wbits else 0
+        rb = 8 - wbits
+        ntz = rnd.choice([4, 5, 5, 5, 6])
+        nk = max(1, (1 << rnd.choice([18, 19, 20])) >> rb)
+        edge = rnd.choice([0, 256, 1 << 16, 1 << 24, None])
+        k0 = rnd.randrange(1, 1 << 30) if edge is None else max(0, edge - rnd.randrange(0, nk))
+        cases.append((nonce, ntz, wb, wbits, k0, k0 + nk))
+    expected = [oracle.mine_window(*c) for c in cases]
+    monkeypatch.setenv("DPOW_DIAG_SHARE_LAUNCH_US", "2")
+    miners = [distpow.Miner(0) for _ in range(4)]
+    monkeypatch.delenv("DPOW_DIAG_SHARE_LAUNCH_US")
+    out, launches = {}, {}
+    try:
+        go = threading.Barrier(4)
+
+        def run(t):
+            go.wait()
+            for i in range(t, len(cases), 4):
+                miners[t].reset_stats()
+                out[i] = miners[t].search(*cases[i])
+                launches[i] = miners[t].stats().launches
+        ths = [threading.Thread(target=run, args=(t,)) for t in range(4)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=60)
+        assert not any(t.is_alive() for t in ths)
+        for i, (c, exp) in enumerate(zip(cases, expected)):
+            r = out[i]
+            if exp is None:
+                assert r.status == EXHAUSTED, (i, c, r)
+            else:
+                assert r.status == FOUND and r.global_idx == exp[1] and list(r.secret) == exp[0], (i, c, r, exp)
+        assert max(launches.values()) >= 4, launches  # the cap cut the windows
+    finally:
+        for m in miners:
+            m.close()
+
+
 def test_n10_min_over_8_partitions(miner, golden):
     """N = 10 on [1,2,3,4] (1.1e12 candidates expected; about 5 s per pass): the minimum of
     the 8 workerBits = 3 partitions' first hits is the workerBits = 0 golden, and the

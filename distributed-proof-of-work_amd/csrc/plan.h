@@ -229,7 +229,10 @@ int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t s
 //  - A grid is sized once per launch, so while the device is shared a launch lasts about
 //    kShareLaunchNs at 1/active of the device's rate (cap_shared_launch): grids follow searches
 //    that start or end beside it.  (One launch per window kept a grid sized for a crowd after
-//    the crowd was gone: the last of 4 searches ran 47 ms on 1 workgroup per CU.)
+//    the crowd was gone: the last of 4 searches ran 47 ms on 1 workgroup per CU.)  8 ms: 8
+//    concurrent searches at 210-212 GH/s with 2 ms launches, 213-214 at 4, 215-216 at 8 and
+//    16 (each launch boundary costs its queue a drain); config 4 over fresh nonces the same
+//    (profiles/r04_share/r04capab/).
 //  - A grid is 1/min(active, kShareMax) of the device (grid_share).  The HIP runtime maps a
 //    process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and the kernels of streams
 //    sharing a queue run one after the other: grids of 1/active left the device part-idle.
@@ -240,7 +243,7 @@ int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t s
 #define DPOW_SHARE_MAX 2
 #endif
 #ifndef DPOW_SHARE_LAUNCH_US
-#define DPOW_SHARE_LAUNCH_US 2000
+#define DPOW_SHARE_LAUNCH_US 8000
 #endif
 constexpr uint64_t kShareMax = DPOW_SHARE_MAX;
 constexpr int64_t kShareLaunchNs = (int64_t)DPOW_SHARE_LAUNCH_US * 1000;

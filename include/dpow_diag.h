@@ -55,7 +55,7 @@ int dpow_diag_dword_test(const uint8_t *nonce, size_t nonce_len, uint32_t ntz, u
  * cap_shared_launch): the device share (cus x the ntz- and size-dependent workgroups per CU
  * / min(share, 2), at least one per claim counter), the expected first hit at ntz, the
  * minimum chunk, the claims per wave and the poll group.  `share` is the number of searches
- * in flight on the device (1 alone); above 1 the window is cut into ~2 ms launches.  One
+ * in flight on the device (1 alone); above 1 the window is cut into ~8 ms launches.  One
  * entry per launch; returns the number of launches (only the first max_launches are
  * written), or < 0 when a launch would leave a claim counter without waves.
  * (ABI 3: ntz, cus and share replace round 3's max_blocks, which sized every launch as an

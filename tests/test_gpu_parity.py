@@ -474,7 +474,7 @@ def test_deep_hits_golden(miner, golden):
 
 def test_concurrent_deep_hits_in_shared_launches(golden):
     """The four config-5 fresh nonces at N = 9 mined at once on one GPU: while the device is
-    shared, dpow_search cuts each window into ~2 ms launches and re-sizes every grid
+    shared, dpow_search cuts each window into ~8 ms launches and re-sizes every grid
     (plan.h grid_share, cap_shared_launch), so each hit (4.5e10-1.1e11 candidates in) lies
     behind hundreds of launch boundaries.  Every answer is still the golden."""
     deep = [e for e in golden["deep_hits"] if e["case"].startswith("config5-fresh")]

@@ -50,7 +50,7 @@ def geometry(nonce, wb, wbits, k0, k1, cus, share=1, ntz=32):
 
 SHARE_MAX = 2  # plan.h kShareMax: a grid is at most 1/2 of the device's however many searches share it
 EST_RATE = 2.3e11  # plan.h kEstRate
-SHARE_LAUNCH_NS = 2_000_000  # plan.h kShareLaunchNs
+SHARE_LAUNCH_NS = 8_000_000  # plan.h kShareLaunchNs
 
 
 def grid_cap(cus, share=1):
@@ -139,7 +139,7 @@ def test_large_and_small_windows():
                 ds = geometry(nonce, wb, wbits, k0, k1, cus, share, ntz)
                 assert (not ds and k1 == 1) or ds[-1].k_end == k1
                 assert all(a.k_end == b.k_begin for a, b in zip(ds, ds[1:]))
-                for d in ds if len(ds) <= 64 else ds[:32] + ds[-32:]:  # a shared device's ~2 ms launches
+                for d in ds if len(ds) <= 64 else ds[:32] + ds[-32:]:  # a shared device's ~8 ms launches
                     check(d, grid_cap(cus, share))
 
 
@@ -168,7 +168,7 @@ def test_chunk_length_spanning_launches(ntz):
         le = lspan_end(ntz, 8 - wbits)
         assert ds[0].k_begin == max(k0, 1) and ds[-1].k_end == k1
         assert all(a.k_end == b.k_begin for a, b in zip(ds, ds[1:]))
-        if share > 1:  # a shared device: launches of at most ~2 ms at 1/share of the rate
+        if share > 1:  # a shared device: launches of at most ~8 ms at 1/share of the rate
             for d in ds:
                 check(d, grid_cap(cus, share))
             continue

@@ -263,10 +263,9 @@ def main():
         # the other ranks wait on a host barrier with their GPUs idle.
         dist.barrier(group=host_group)
         if rank == 0:
-            ndev = max(1, torch.cuda.device_count())  # the GPUs this process sees
             try:
                 extra["coordinator_node"] = coordinator_configs(
-                    devices=[0] * world if args.same_device else [i % ndev for i in range(world)])
+                    devices=node_devices(world, args.same_device, torch.cuda.device_count()))
             except Exception as e:  # reported, not fatal: the sweep line above is the benchmark
                 log(f"rank 0: coordinator configs in the node shape failed: {e!r}")
                 extra["coordinator_node"] = {"error": repr(e)}
@@ -521,6 +520,13 @@ def collective_probe(miner, rank, world, dev, board, backend, reps=200):
                              if vote else None),
             "batch_2p16_candidates_us": {"median": med(batch), "p90": round(sorted(batch)[int(len(batch) * 0.9)], 1)},
             "node_mine": tts}
+
+
+def node_devices(world, same_device, visible):
+    """The GPU of logical worker i in the node-shape coordinator configs: rank i's GPU (i), on
+    the GPUs this process sees (`visible`, at least one); all on GPU 0 for --same-device."""
+    n = max(1, visible)
+    return [0] * world if same_device else [i % n for i in range(world)]
 
 
 def coordinator_configs(devices=(0,)):

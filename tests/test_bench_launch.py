@@ -74,3 +74,14 @@ def test_failing_ranks_fail_the_bench():
     assert r.returncode != 0, (r.stdout, r.stderr[-2000:])
     assert r.stdout == ""
     assert "torch.distributed.run" in r.stderr  # the launcher ran
+
+
+def test_node_shape_coordinator_devices():
+    """bench.py's node-shape BASELINE configs put logical worker i on rank i's GPU, wrapping
+    onto the GPUs the process sees, and everything on GPU 0 for --same-device rehearsals."""
+    import bench
+    assert bench.node_devices(8, False, 8) == list(range(8))
+    assert bench.node_devices(4, False, 8) == [0, 1, 2, 3]
+    assert bench.node_devices(8, False, 2) == [0, 1] * 4
+    assert bench.node_devices(2, False, 0) == [0, 0]
+    assert bench.node_devices(8, True, 8) == [0] * 8

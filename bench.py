@@ -21,10 +21,12 @@ on the search stream), time-to-secret for the BASELINE configs, and the CPU
 baseline (the oracle's restatement of the reference Go loop on the host cores).
 """
 import argparse
+import datetime
 import json
 import math
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -50,6 +52,9 @@ TTS_RUNS = 3                       # time-to-secret: median of 3 searches (first
 NODE_SYNC = os.environ.get("DPOW_NODE_ASYNC") != "1"
 # N > 1: the node's shared-memory Found fan-out (NodeBoard) unless DPOW_NODE_BOARD=0
 NODE_BOARD = os.environ.get("DPOW_NODE_BOARD") != "0"
+# host (gloo) barriers and votes between the sections: a rank lost inside one ends the others'
+# wait after this long, with an error in the line, instead of RCCL's 10-minute timeout
+HOST_TIMEOUT_S = 180
 OPS_PER_CANDIDATE = 256           # algorithmic INT32 ops: 64 MD5 steps x {bool3, add3, rotate, add}
 # INT32 VALU issue peak of gfx950: 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s,
 # the MI355X_MICROARCH.md FP32 vector peak (157.3 TFLOP/s) / 2 FLOP per FMA lane-op.
@@ -60,7 +65,105 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
+class TorchGPU:
+    """The few device operations the bench makes outside libdpow (torch's HIP runtime): the
+    current device, a device-wide synchronize, and HIP events on the search stream.  A test
+    may pass a CPU stand-in to main() (tests/test_bench_sections.py)."""
+    available = True
+
+    def set_device(self, device):
+        torch.cuda.set_device(device)
+
+    def synchronize(self):
+        torch.cuda.synchronize()
+
+    def stream_timer(self, miner):
+        return _StreamTimer(miner)
+
+
+class _StreamTimer:
+    """HIP events on the search stream (torch.cuda.Event sees only torch's current stream)."""
+
+    def __init__(self, miner):
+        self.ext = torch.cuda.ExternalStream(miner.stream_handle())
+        self.ev0, self.ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def start(self):
+        self.ev0.record(self.ext)
+
+    def stop(self):
+        self.ev1.record(self.ext)
+
+    def elapsed_ms(self):
+        return self.ev0.elapsed_time(self.ev1)
+
+
+class LineGuard:
+    """Rank 0's one JSON line, printed exactly once: at the end, or with what was measured so
+    far when the launcher stops this rank before the end (torch.distributed.run sends SIGTERM
+    to the other ranks when one fails).  The signal's handler only runs in the main thread, which
+    may be blocked inside a collective then; so the C-level handler's wakeup byte
+    (signal.set_wakeup_fd) is read by a watcher thread, which prints the line and exits."""
+
+    def __init__(self):
+        self.line = None
+        self.printed = False
+        self.lock = threading.Lock()
+
+    def arm(self, line):
+        import signal
+        with self.lock:
+            self.line = line
+        r, w = os.pipe()
+        os.set_blocking(w, False)
+        signal.signal(signal.SIGTERM, lambda *a: None)  # a Python-level handler: the wakeup byte is written
+        signal.set_wakeup_fd(w)
+        threading.Thread(target=self._watch, args=(r,), daemon=True).start()
+
+    def _watch(self, r):
+        import signal
+        while True:
+            b = os.read(r, 1)
+            if b and b[0] in (signal.SIGTERM, signal.SIGINT):
+                self.emit({"ok": False, "error": f"rank 0 stopped by signal {b[0]} before the end "
+                                                 "(another rank failed?): the sections not listed did not finish"})
+                os._exit(128 + b[0])
+
+    def update(self, key, value):
+        with self.lock:
+            if self.line is not None:
+                self.line[key] = value
+
+    def emit(self, extra=None):
+        with self.lock:
+            if self.printed or self.line is None:
+                return
+            self.printed = True
+            line = dict(self.line, **(extra or {}))
+            sys.stdout.write(json.dumps(line) + "\n")
+            sys.stdout.flush()
+
+
+def section(name, rank, fn, *a, **kw):
+    """One bench section after the sweep: a failure becomes {"error": ...} in the line instead of
+    an exception that would lose the sweep's number."""
+    try:
+        return fn(*a, **kw)
+    except Exception as e:
+        log(f"rank {rank}: bench section {name} failed: {e!r}")
+        return {"error": repr(e)}
+
+
+def section_ok(v):
+    """False when a section (or a case in it) failed or returned a wrong answer."""
+    if isinstance(v, dict):
+        if "error" in v or v.get("ok") is False:
+            return False
+        return all(section_ok(x) for x in v.values())
+    return True
+
+
+def main(argv=None, miner_factory=None, gpu=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -82,7 +185,9 @@ def main():
                     help="rehearsal: every rank searches on device 0 (with --backend gloo)")
     ap.add_argument("--print-launch", action="store_true",
                     help="print the rank launcher's command (--gpus N > 1 without WORLD_SIZE) as JSON and exit")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    gpu = gpu or TorchGPU()
+    miner_factory = miner_factory or distpow.Miner
 
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
@@ -99,18 +204,20 @@ def main():
         log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the command line disagree")
         sys.exit(2)
     device = 0 if args.same_device else local_rank
-    torch.cuda.set_device(device)
+    gpu.set_device(device)
     tick_group = None
-    host_group = None  # world > 1 over RCCL: a gloo group; else the default group
+    host_group = None  # host-only (gloo) barriers and votes between the sections
     dist_on = world > 1 or not args.no_dist
     if world > 1:
         if args.backend == "nccl":  # RCCL over xGMI
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
             if not NODE_SYNC:  # node_mine_async's ticks: a host (gloo) group, off the busy GPUs
                 tick_group = dist.new_group(backend="gloo")
-            host_group = dist.new_group(backend="gloo")  # host-only barriers (no GPU kernel waits)
+            # host-only barriers (no GPU kernel waits), bounded: a rank lost inside a section
+            # ends the others' wait with an error instead of holding the bench for RCCL's 10 min
+            host_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=HOST_TIMEOUT_S))
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=HOST_TIMEOUT_S))
     elif dist_on:
         # One GPU: a world-1 RCCL group all the same, so the N = 1 line runs the code path of
         # the N-GPU node -- the per-step all-reduce and node_mine's batch boundaries over RCCL.
@@ -122,15 +229,14 @@ def main():
     board = None
     if world > 1 and NODE_BOARD:
         try:
-            board = NodeBoard.create()  # None when the ranks do not share one host
+            board = NodeBoard.create(host_group)  # None when the ranks do not share one host
         except Exception as e:  # the node search stays correct without it (batch boundaries only)
             log(f"rank {rank}: no node board ({e!r}); node_mine runs on batch boundaries alone")
             board = None
         # every rank must agree on using it (node_mine's collectives stay matched either way,
         # but the board's slot reset schedule assumes all ranks call it)
-        have = torch.tensor([1 if board is not None else 0], dtype=torch.int64,
-                            device=torch.device("cuda", device) if args.backend == "nccl" else "cpu")
-        dist.all_reduce(have, op=dist.ReduceOp.MIN)
+        have = torch.tensor([1 if board is not None else 0], dtype=torch.int64)
+        dist.all_reduce(have, op=dist.ReduceOp.MIN, group=host_group)
         if int(have.item()) == 0 and board is not None:
             board.close()
             board = None
@@ -142,10 +248,10 @@ def main():
     # dpow_open: the first one in the process loads every search kernel on the device
     # ("Search start"); a second one does not
     t_open = time.perf_counter()
-    miner = distpow.Miner(device)
+    miner = miner_factory(device)
     open_ms = [(time.perf_counter() - t_open) * 1e3]
     t_open = time.perf_counter()
-    distpow.Miner(device).close()
+    miner_factory(device).close()
     open_ms.append((time.perf_counter() - t_open) * 1e3)
     dev = torch.device("cuda", device) if args.backend == "nccl" else torch.device("cpu")
     red = torch.empty(2, dtype=torch.int64, device=dev)
@@ -157,7 +263,8 @@ def main():
     def step(s):
         k_begin = K0 + (s % n_windows) * batch_k
         r = miner.search(NONCE, SWEEP_NTZ, wb, wbits, k_begin, k_begin + batch_k)
-        assert r.status == distpow.EXHAUSTED, r  # N = 32 is unreachable in 2^36 candidates
+        if r.status != distpow.EXHAUSTED:  # N = 32 is unreachable in 2^36 candidates
+            raise RuntimeError(f"sweep step {s}: status {r.status}, expected EXHAUSTED")
         if dist_on:
             red[0] = r.global_idx if r.status == distpow.FOUND else distpow.DPOW_NO_HIT
             red[1] = 1
@@ -165,27 +272,26 @@ def main():
 
     def barrier():
         if dist_on:
-            dist.barrier()
-        torch.cuda.synchronize()
+            dist.barrier(group=host_group)
+        gpu.synchronize()
 
     for s in range(args.warmup):
         step(s)
     miner.reset_stats()
-    ext = torch.cuda.ExternalStream(miner.stream_handle())
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    timer = gpu.stream_timer(miner)
     barrier()
     t0 = time.perf_counter()
-    ev0.record(ext)
+    timer.start()
     for s in range(args.warmup, args.warmup + args.steps):
         step(s)
-    ev1.record(ext)
+    timer.stop()
     barrier()
     elapsed = time.perf_counter() - t0
     st = miner.stats()
-    stream_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    stream_ms = timer.elapsed_ms()
+    t = torch.tensor([elapsed], dtype=torch.float64)
     if dist_on:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=host_group)
     elapsed_max = float(t.item())
 
     total_candidates = world * per_gpu * args.steps
@@ -198,96 +304,129 @@ def main():
     record_launch_ms = st.kernel_ms / max(1, st.launches)
     cand_per_launch = st.candidates / max(1, st.launches)
     achieved_tops = cand_per_launch * OPS_PER_CANDIDATE / (avg_launch_ms * 1e-3) / 1e12
-    kernel_ghs = st.candidates / (st.kernel_ms * 1e-3) / 1e9
+    kernel_ghs = st.candidates / max(1e-12, st.kernel_ms * 1e-3) / 1e9
 
-    # time-to-secret for the BASELINE configs (deterministic answers; node-wide when world > 1):
-    # search_ms = the search call (what a worker reports), ms = up to the device synchronize
-    # after it (it also waits out launches still queued behind the hit), and at N > 1 the
-    # barrier after it (the slowest rank)
-    tts = {}
-    extra = {}
-    ttsk = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8),
-            ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5)]
-    # BASELINE config 5: N = 9 on fresh 4-byte nonces seeded random.Random(416)
-    ttsk += [(n, 9) for n in config5_fresh_nonces()]
-    for nonce, n in ([] if args.no_tts else ttsk):
-        runs, search_runs = [], []
-        for _ in range(TTS_RUNS):
-            barrier()
-            t1 = time.perf_counter()
-            if world == 1:  # one rank: the miner's own pipelined windows, no batch boundaries
-                r = miner.mine(nonce, n)
-                res = NodeResult(r.status, r.global_idx, r.secret, 0, 0)
-            elif NODE_SYNC:  # batch-synchronous node search, Found fan-out through the node board
-                res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world, device=dev,
-                                board=board, attach_fn=miner.attach_node)
-            else:  # no batch boundaries: ticked all-reduce + the node's best injected into each rank's search
-                res = node_mine_async(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
-                                      bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
-                                      device=dev, tick_group=tick_group)
-            search_runs.append((time.perf_counter() - t1) * 1e3)
-            if world > 1:
-                barrier()
-            else:  # one rank: the device drained (launches still queued behind the hit retire)
-                torch.cuda.synchronize()
-            runs.append((time.perf_counter() - t1) * 1e3)
-            assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
-        tts[f"{bytes(nonce).hex()}/{n}"] = {"ms": round(sorted(runs)[len(runs) // 2], 3),
-                                            "search_ms": round(sorted(search_runs)[len(search_runs) // 2], 3),
-                                            "first_ms": round(runs[0], 3), "global_idx": res.global_idx,
-                                            "secret": list(res.secret)}
+    # The line holds the sweep from here on: every later section adds to it or records its error.
+    guard = LineGuard()
+    if rank == 0:
+        cus, bpc, tpb = miner.geometry()
+        guard.arm(sweep_line(args, world, wbits, per_gpu, batch_k, value, elapsed_max, kernel_ghs, achieved_tops,
+                             avg_launch_ms, record_launch_ms, cand_per_launch, st, stream_ms, open_ms, cus, tpb))
+
+    # time-to-secret for the BASELINE configs (deterministic answers; node-wide when world > 1)
+    if not args.no_tts:
+        guard.update("time_to_secret", section("time_to_secret", rank, time_to_secret, miner, rank, world, dev, board,
+                                               barrier, gpu))
+        guard.update("time_to_secret_node_search",
+                     "one rank: Miner.mine" if world == 1 else
+                     ("node_mine (batch-synchronous, node board)" if board is not None
+                      else "node_mine (batch-synchronous)") if NODE_SYNC else
+                     "node_mine_async (ticked all-reduce, bound injection)")
 
     # The node's collective path at this world size: the batch boundary of node_mine
     # (host -> device copy, RCCL MIN all-reduce, device -> host copy, synchronize), and
     # node_mine over Miner.search for two BASELINE cases.
     if dist_on and not args.no_tts:
-        extra["collective"] = collective_probe(miner, rank, world, dev, board, args.backend)
+        guard.update("collective", section("collective", rank, collective_probe, miner, rank, world, dev, board,
+                                           args.backend, gpu))
 
     # Secondary sweep: the whole L = 3 chunk segment, k in [2^16, 2^24),
     # one variable message word; and the early-exit latency of a Found/Cancel (worker.go:194,209).
     if not args.no_tts:
         barrier()
-        miner.reset_stats()
-        assert miner.search(NONCE, SWEEP_NTZ, wb, wbits, 1 << 16, 1 << 24).status == distpow.EXHAUSTED
-        s3 = miner.stats()
-        extra["secondary_sweep"] = {
-            "workload": "L=3 chunk segment, k in [2^16, 2^24), this rank's partition, N=32",
-            "candidates": int(s3.candidates), "kernel_ghs": round(s3.candidates / (s3.kernel_ms * 1e-3) / 1e9, 3)}
-        extra["cancel_latency_ms"] = cancel_latency(miner)
+        guard.update("secondary_sweep", section("secondary_sweep", rank, secondary_sweep, miner, wb, wbits))
+        guard.update("cancel_latency_ms", section("cancel_latency", rank, cancel_latency, miner, gpu))
 
     if rank == 0 and world == 1 and not args.no_tts:
-        extra["coordinator"] = coordinator_configs()
+        guard.update("coordinator", section("coordinator", rank, coordinator_configs))
     if world > 1 and not args.no_tts:
         # BASELINE configs 3-5 in their node shape: rank 0's process runs the coordinator mirror
         # with logical worker i on GPU i % world (coordinator.go:139-298 over W machines), while
         # the other ranks wait on a host barrier with their GPUs idle.
         dist.barrier(group=host_group)
         if rank == 0:
-            try:
-                extra["coordinator_node"] = coordinator_configs(
-                    devices=node_devices(world, args.same_device, torch.cuda.device_count()))
-            except Exception as e:  # reported, not fatal: the sweep line above is the benchmark
-                log(f"rank 0: coordinator configs in the node shape failed: {e!r}")
-                extra["coordinator_node"] = {"error": repr(e)}
+            guard.update("coordinator_node", section(
+                "coordinator_node", rank, coordinator_configs,
+                devices=node_devices(world, args.same_device, torch.cuda.device_count())))
         dist.barrier(group=host_group)
 
     probe = {}
     if rank == 0 and not args.no_probe:
-        from distpow._lib import VALU_KINDS, valu_rate
-        for kind, name in VALU_KINDS.items():
-            r, clk = valu_rate(device, kind)
-            probe[name] = {"tops": round(r / 1e12, 3), "clock_ghz": round(clk, 3)}
+        probe = section("valu_probe", rank, valu_probe, device)
+    guard.update("valu_probe", probe)
 
-    cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_threads, args.cpu_seconds)
+        guard.update("cpu_baseline", section("cpu_baseline", rank, cpu_baseline, args.cpu_threads, args.cpu_seconds))
 
-    # Memory traffic and the PMC issue model per sweep launch, from the committed rocprofv3
-    # summary (tools/profile_gpu.sh + tools/summarize_profile.py) of THIS build: the
-    # profiles/*_summary.json whose build_id is distpow.build_id(); none -> null, with the
-    # reason.  Traffic is uncorrected: the search reads no data, so these bytes are kernarg
-    # scalar loads, the claim atomics and the completion records -- not algorithmic HBM
-    # traffic (that is 0 per candidate).
+    if rank == 0:
+        guard.update("roofline", dict(guard.line["roofline"], **roofline_profile(probe, achieved_tops)))
+        guard.update("ok", all(section_ok(guard.line.get(k)) for k in
+                               ("time_to_secret", "collective", "secondary_sweep", "cancel_latency_ms", "coordinator",
+                                "coordinator_node", "valu_probe", "cpu_baseline")))
+        guard.emit()
+    miner.close()
+    if board is not None:
+        try:
+            board.close()
+        except Exception as e:
+            log(f"rank {rank}: board close: {e!r}")
+    if dist_on:
+        dist.destroy_process_group()
+
+
+def sweep_line(args, world, wbits, per_gpu, batch_k, value, elapsed_max, kernel_ghs, achieved_tops, avg_launch_ms,
+               record_launch_ms, cand_per_launch, st, stream_ms, open_ms, cus, tpb):
+    """The bench line as the sweep alone gives it (the sections after it add their entries)."""
+    return {
+        "metric": "MD5 candidates/sec (GH/s), whole node",
+        "value": round(value, 3),
+        "unit": "GH/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {
+            "workload": "sweep: nonce [1,2,3,4], 32 trailing zeros (unreachable), "
+                        + ("2^38 candidates per step over all GPUs" if args.strong else "2^36 candidates per GPU per step")
+                        + " in the L=4 chunk segment (k >= 2^24); per-step RCCL MIN all-reduce",
+            "nonce": NONCE, "ntz": SWEEP_NTZ, "candidates_per_gpu_per_step": per_gpu,
+            "k_window_per_step": batch_k, "parallelism": f"prefix-partition x{world} (workerBits={wbits})",
+        },
+        "per_gpu_ghs": round(value / world, 3),
+        "kernel_ghs": round(kernel_ghs, 3),
+        "roofline": {
+            "bound": "valu",
+            "achieved": round(achieved_tops, 3),
+            "peak": round(PEAK_TOPS, 3),
+            "unit": "TOP/s (INT32 VALU lane-ops)",
+            "frac": round(achieved_tops / PEAK_TOPS, 4),
+            "traffic": None,
+            "ops_per_candidate": OPS_PER_CANDIDATE,
+            "avg_launch_ms": round(avg_launch_ms, 4),
+            "avg_launch_ms_source": "HIP events on the search stream around the timed steps / launches",
+            "avg_launch_ms_in_kernel": round(record_launch_ms, 4),
+            "candidates_per_launch": int(cand_per_launch),
+            "launches": int(st.launches),
+        },
+        "stream_event_ms": round(stream_ms, 3),
+        "dpow_open_ms": {"first": round(open_ms[0], 3), "again": round(open_ms[1], 3)},
+        "geometry": {"cus": cus, "threads_per_block": tpb},
+        "build_id": distpow.build_id(),  # = the sources' hash (distpow._lib.check_build refused anything else)
+    }
+
+
+def roofline_profile(probe, achieved_tops):
+    """Memory traffic and the PMC issue model per sweep launch, from the committed rocprofv3
+    summary (tools/profile_gpu.sh + tools/summarize_profile.py) of THIS build: the
+    profiles/*_summary.json whose build_id is distpow.build_id(); none -> null, with the
+    reason.  Traffic is uncorrected: the search reads no data, so these bytes are kernarg
+    scalar loads, the claim atomics and the completion records -- not algorithmic HBM
+    traffic (that is 0 per candidate)."""
     traffic, traffic_src, issue, prof_reason = None, None, None, None
     ps, prof = profile_summary_of(distpow.build_id())
     if ps is None:
@@ -309,72 +448,87 @@ def main():
                            "claim atomics + kernarg loads, no algorithmic HBM bytes")
     # The box's shader clock under full VALU load, from this run's issue-rate probe: frac is
     # priced at the 2.4 GHz spec clock, and boxes run 2.30-2.36 GHz under this load.
-    box_clk = (probe.get("md5_step_mix") or {}).get("clock_ghz")
+    box_clk = (probe.get("md5_step_mix") or {}).get("clock_ghz") if isinstance(probe, dict) else None
+    return {
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "issue": issue,
+        "profile_reason": prof_reason,
+        "box_clock_ghz": box_clk,
+        "box_clock_source": "dpow_diag_valu_rate md5_step_mix probe of this run (all CUs busy)" if box_clk else None,
+        "frac_at_box_clock": (round(achieved_tops / (256 * 4 * 32 * box_clk * 1e9 / 1e12), 4) if box_clk else None),
+    }
 
-    if rank == 0:
-        cus, bpc, tpb = miner.geometry()
-        out = {
-            "metric": "MD5 candidates/sec (GH/s), whole node",
-            "value": round(value, 3),
-            "unit": "GH/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic",
-            "config": {
-                "workload": "sweep: nonce [1,2,3,4], 32 trailing zeros (unreachable), "
-                            + ("2^38 candidates per step over all GPUs" if args.strong else "2^36 candidates per GPU per step")
-                            + " in the L=4 chunk segment (k >= 2^24); per-step RCCL MIN all-reduce",
-                "nonce": NONCE, "ntz": SWEEP_NTZ, "candidates_per_gpu_per_step": per_gpu,
-                "k_window_per_step": batch_k, "parallelism": f"prefix-partition x{world} (workerBits={wbits})",
-            },
-            "per_gpu_ghs": round(value / world, 3),
-            "kernel_ghs": round(kernel_ghs, 3),
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved_tops, 3),
-                "peak": round(PEAK_TOPS, 3),
-                "unit": "TOP/s (INT32 VALU lane-ops)",
-                "frac": round(achieved_tops / PEAK_TOPS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "ops_per_candidate": OPS_PER_CANDIDATE,
-                "avg_launch_ms": round(avg_launch_ms, 4),
-                "avg_launch_ms_source": "HIP events on the search stream around the timed steps / launches",
-                "avg_launch_ms_in_kernel": round(record_launch_ms, 4),
-                "candidates_per_launch": int(cand_per_launch),
-                "launches": int(st.launches),
-                "issue": issue,
-                "profile_reason": prof_reason,
-                "box_clock_ghz": box_clk,
-                "box_clock_source": "dpow_diag_valu_rate md5_step_mix probe of this run (all CUs busy)" if box_clk else None,
-                "frac_at_box_clock": (round(achieved_tops / (256 * 4 * 32 * box_clk * 1e9 / 1e12), 4)
-                                      if box_clk else None),
-            },
-            "stream_event_ms": round(stream_ms, 3),
-            "dpow_open_ms": {"first": round(open_ms[0], 3), "again": round(open_ms[1], 3)},
-            "valu_probe": probe,
-            "time_to_secret": tts,
-            "time_to_secret_node_search": ("one rank: Miner.mine" if world == 1 else
-                                           ("node_mine (batch-synchronous, node board)" if board is not None
-                                            else "node_mine (batch-synchronous)") if NODE_SYNC else
-                                           "node_mine_async (ticked all-reduce, bound injection)"),
-            **extra,
-            "cpu_baseline": cpu,
-            "geometry": {"cus": cus, "threads_per_block": tpb},
-            "build_id": distpow.build_id(),  # = the sources' hash (distpow._lib.check_build refused anything else)
-        }
-        print(json.dumps(out), flush=True)
-    miner.close()
-    if board is not None:
-        board.close()
-    if dist_on:
-        dist.destroy_process_group()
+
+def valu_probe(device):
+    from distpow._lib import VALU_KINDS, valu_rate
+    probe = {}
+    for kind, name in VALU_KINDS.items():
+        r, clk = valu_rate(device, kind)
+        probe[name] = {"tops": round(r / 1e12, 3), "clock_ghz": round(clk, 3)}
+    return probe
+
+
+def time_to_secret(miner, rank, world, dev, board, barrier, gpu):
+    """Time-to-secret of the BASELINE configs: search_ms = the search call (what a worker
+    reports), ms = up to the device synchronize after it (it also waits out launches still
+    queued behind the hit), and at N > 1 the barrier after it (the slowest rank).  A wrong
+    answer is recorded ("ok": false), not raised.  A failed node search is voted on every
+    rank (node_mine's healthy vote), so all ranks leave this section at the same case."""
+    tts = {}
+    ttsk = [([1, 2, 3, 4], 3), ([1, 2, 3, 4], 6), ([1, 2, 3, 4], 7), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8),
+            ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5)]
+    # BASELINE config 5: N = 9 on fresh 4-byte nonces seeded random.Random(416) (SURVEY.md 8(d) item 5)
+    ttsk += [(n, 9) for n in config5_fresh_nonces()]
+    for nonce, n in ttsk:
+        key = f"{bytes(nonce).hex()}/{n}"
+        runs, search_runs, wrong = [], [], []
+        try:
+            for _ in range(TTS_RUNS):
+                barrier()
+                t1 = time.perf_counter()
+                if world == 1:  # one rank: the miner's own pipelined windows, no batch boundaries
+                    r = miner.mine(nonce, n)
+                    res = NodeResult(r.status, r.global_idx, r.secret, 0, 0)
+                elif NODE_SYNC:  # batch-synchronous node search, Found fan-out through the node board
+                    res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world, device=dev,
+                                    board=board, attach_fn=miner.attach_node)
+                else:  # no batch boundaries: ticked all-reduce + the node's best injected into each rank's search
+                    res = node_mine_async(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
+                                          bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
+                                          device=dev)
+                search_runs.append((time.perf_counter() - t1) * 1e3)
+                if world > 1:
+                    barrier()
+                else:  # one rank: the device drained (launches still queued behind the hit retire)
+                    gpu.synchronize()
+                runs.append((time.perf_counter() - t1) * 1e3)
+                if not (res.status == distpow.FOUND and res.secret is not None and distpow.verify(nonce, res.secret, n)):
+                    wrong.append({"status": res.status, "global_idx": res.global_idx,
+                                  "secret": list(res.secret) if res.secret else None})
+        except Exception as e:  # voted: every rank stops here; the cases before it stay in the line
+            log(f"rank {rank}: time-to-secret {key} failed: {e!r}")
+            tts[key] = {"ok": False, "error": repr(e)}
+            tts["error"] = f"{key}: {e!r}"
+            break
+        tts[key] = {"ms": round(sorted(runs)[len(runs) // 2], 3),
+                    "search_ms": round(sorted(search_runs)[len(search_runs) // 2], 3),
+                    "first_ms": round(runs[0], 3), "global_idx": res.global_idx,
+                    "secret": list(res.secret) if res.secret else None}
+        if wrong:
+            tts[key].update(ok=False, wrong=wrong)
+    return tts
+
+
+def secondary_sweep(miner, wb, wbits):
+    miner.reset_stats()
+    r = miner.search(NONCE, SWEEP_NTZ, wb, wbits, 1 << 16, 1 << 24)
+    s3 = miner.stats()
+    out = {"workload": "L=3 chunk segment, k in [2^16, 2^24), this rank's partition, N=32",
+           "candidates": int(s3.candidates), "kernel_ghs": round(s3.candidates / max(1e-12, s3.kernel_ms * 1e-3) / 1e9, 3)}
+    if r.status != distpow.EXHAUSTED:
+        out.update(ok=False, status=r.status)
+    return out
 
 
 def profile_summary_of(build):
@@ -454,15 +608,17 @@ def launch_ranks(args):
     return rc
 
 
-def collective_probe(miner, rank, world, dev, board, backend, reps=200):
+def collective_probe(miner, rank, world, dev, board, backend, gpu, reps=200):
     """node_mine's batch boundary on this node's process group (RCCL with the nccl backend):
     median us of [pinned host -> device copy, all-reduce MIN of 3 int64, device -> host
     copy, stream synchronize] -- the per-batch cost c the expected-time batch of
     node.auto_batch_candidates assumes -- and, with a shared node board, of the node vote
     that replaces it there (NodeBoard.vote, all ranks on one host); of one whole node_mine
     batch over a window of 2^16 candidates per rank (the search call plus the boundary),
-    and node_mine's time-to-secret for two BASELINE cases over this group."""
+    and node_mine's time-to-secret for two BASELINE cases over this group.  Wrong values are
+    recorded (wrong: [...]), not raised, so every rank runs the same collectives."""
     on_gpu = dev.type == "cuda"
+    wrong = []
     buf = torch.zeros(3, dtype=torch.int64, device=dev)
     hbuf = torch.zeros(3, dtype=torch.int64, pin_memory=on_gpu)
     lat = []
@@ -485,7 +641,9 @@ def collective_probe(miner, rank, world, dev, board, backend, reps=200):
         for i in range(reps + 10):
             dist.barrier()
             t = time.perf_counter()
-            assert board.vote([i, 1, 1]) == [i, 1, 1]
+            v = board.vote([i, 1, 1])
+            if v != [i, 1, 1]:
+                wrong.append(f"node vote {i}: {v}")
             if i >= 10:
                 vote.append((time.perf_counter() - t) * 1e6)
     wb, wbits = partition_of_rank(rank, world)
@@ -494,27 +652,29 @@ def collective_probe(miner, rank, world, dev, board, backend, reps=200):
     batch = []
     for i in range(60):
         dist.barrier()
-        torch.cuda.synchronize()
+        gpu.synchronize()
         t = time.perf_counter()
         r = node_mine(search, NONCE, SWEEP_NTZ, rank, world, batch_k=(1 << 16) // R, k_start=K0 + i * (1 << 16) // R,
                       k_limit=K0 + (i + 1) * (1 << 16) // R, device=dev)
         if i >= 10:
             batch.append((time.perf_counter() - t) * 1e6)
-        assert r.status == distpow.EXHAUSTED and r.batches == 1
+        if not (r.status == distpow.EXHAUSTED and r.batches == 1):
+            wrong.append(f"batch {i}: status {r.status}, {r.batches} batches")
     tts = {}
     for nonce, n in (([1, 2, 3, 4], 6), ([1, 2, 3, 4], 8)):
         ms = []
         for _ in range(TTS_RUNS):
             dist.barrier()
-            torch.cuda.synchronize()
+            gpu.synchronize()
             t = time.perf_counter()
             res = node_mine(search, nonce, n, rank, world, device=dev, board=board, attach_fn=miner.attach_node)
             ms.append((time.perf_counter() - t) * 1e3)
-            assert res.status == distpow.FOUND and distpow.verify(nonce, res.secret, n)
+            if not (res.status == distpow.FOUND and res.secret is not None and distpow.verify(nonce, res.secret, n)):
+                wrong.append(f"node_mine {bytes(nonce).hex()}/{n}: status {res.status}, index {res.global_idx}")
         tts[f"{bytes(nonce).hex()}/{n}"] = {"search_ms": round(sorted(ms)[len(ms) // 2], 3),
                                             "global_idx": res.global_idx, "batches": res.batches}
     med = lambda v: round(sorted(v)[len(v) // 2], 1)  # noqa: E731
-    return {"backend": backend, "world": world,
+    return {"backend": backend, "world": world, **({"ok": False, "wrong": wrong} if wrong else {}),
             "batch_boundary_us": {"median": med(lat), "p90": round(sorted(lat)[int(len(lat) * 0.9)], 1)},
             "node_vote_us": ({"median": med(vote), "p90": round(sorted(vote)[int(len(vote) * 0.9)], 1)}
                              if vote else None),
@@ -540,7 +700,8 @@ def coordinator_configs(devices=(0,)):
     def timed(c, nonce, n):
         t = time.perf_counter()
         s = c.mine(nonce, n)
-        assert distpow.verify(nonce, s, n)
+        if not distpow.verify(nonce, s, n):
+            raise RuntimeError(f"coordinator: {bytes(nonce).hex()}/{n} returned {list(s)}, which does not verify")
         return round((time.perf_counter() - t) * 1e3, 3)
 
     devices = list(devices)
@@ -564,7 +725,8 @@ def coordinator_configs(devices=(0,)):
             x.start()
         for x in th:
             x.join(120)
-        assert len(done) == 4
+        if len(done) != 4:
+            raise RuntimeError(f"config 5: {len(done)} of 4 client requests finished within 120 s")
         out["config5_two_clients_total_ms"] = round((time.perf_counter() - t) * 1e3, 3)
     # Config 4's one nonce times one draw (which worker holds the first hit, and the share of the
     # device its search got); over fresh nonces the mean follows the device's aggregate rate.
@@ -592,12 +754,17 @@ def shared_device_rate(w, device=0, span=26):
         for _ in range(3):  # median of 3
             go = threading.Barrier(w + 1)
             ends = [0.0] * w
+            errors = []
 
             def run(i):
-                go.wait()
-                r = miners[i].search(NONCE, 32, i, bits, 1 << 24, (1 << 24) + (1 << span))
-                assert r.status == distpow.EXHAUSTED
-                ends[i] = time.perf_counter()
+                try:
+                    go.wait()
+                    r = miners[i].search(NONCE, 32, i, bits, 1 << 24, (1 << 24) + (1 << span))
+                    if r.status != distpow.EXHAUSTED:
+                        raise RuntimeError(f"search {i}: status {r.status}, expected EXHAUSTED")
+                    ends[i] = time.perf_counter()
+                except BaseException as e:  # reported below, never a rate from the survivors alone
+                    errors.append(repr(e))
             th = [threading.Thread(target=run, args=(i,)) for i in range(w)]
             for x in th:
                 x.start()
@@ -605,6 +772,8 @@ def shared_device_rate(w, device=0, span=26):
             t0 = time.perf_counter()
             for x in th:
                 x.join(60)
+            if errors or any(x.is_alive() for x in th) or min(ends) <= 0.0:
+                raise RuntimeError(f"shared-device rate: {errors or 'a search did not finish within 60 s'}")
             rates.append(w * ((1 << span) << (8 - bits)) / (max(ends) - t0) / 1e9)
         return round(sorted(rates)[1], 1)
     finally:
@@ -612,7 +781,7 @@ def shared_device_rate(w, device=0, span=26):
             m.close()
 
 
-def cancel_latency(miner, reps=3, run_s=0.05):
+def cancel_latency(miner, gpu, reps=3, run_s=0.05):
     """Median ms from raising the pinned cancel flag (what Found/Cancel do, worker.go:194,209)
     to dpow_search returning CANCELLED, mid-way through a 2.8e14-candidate window."""
     import threading
@@ -627,9 +796,10 @@ def cancel_latency(miner, reps=3, run_s=0.05):
         miner.cancel()
         th.join(timeout=30)
         miner.clear_cancel()
-        assert not th.is_alive() and out["r"].status == distpow.CANCELLED, out
+        if th.is_alive() or out["r"].status != distpow.CANCELLED:
+            raise RuntimeError(f"cancel did not stop the search within 30 s: {out}")
         lat.append((out["t"] - t0) * 1e3)
-    torch.cuda.synchronize()
+    gpu.synchronize()
     return round(sorted(lat)[len(lat) // 2], 3)
 
 

@@ -239,14 +239,25 @@ class NodeBoard:
         end); the library drops its HIP registration of the pages (dpow_node_release), so a
         later board mapped at the same address is registered afresh."""
         if self._shm is not None:
-            from ._lib import check, lib
-            check(lib().dpow_node_release(self._base, self.nbytes(self.world)), "dpow_node_release")
-            self._base = 0
+            from ._lib import DpowError, check, lib
+            err = None
             try:
-                self._shm.close()
-            except BufferError:  # a ctypes view still alive; the mapping goes with the process
-                pass
+                check(lib().dpow_node_release(self._base, self.nbytes(self.world)), "dpow_node_release")
+            except DpowError as e:
+                # A context still attached (a failed search skipped its detach): the pages stay
+                # registered, so the mapping is left to the process -- unmapping it under a
+                # registration would let a later mapping at the same address match it.  The
+                # error is raised after the cleanup, so it never hides the one that led here.
+                err = e
+            self._base = 0
+            if err is None:
+                try:
+                    self._shm.close()
+                except BufferError:  # a ctypes view still alive; the mapping goes with the process
+                    pass
             self._shm = None
+            if err is not None:
+                raise err
 
 
 # With a node board, hits end every rank's batch at once, so a batch costs its boundary
@@ -319,19 +330,31 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
     slot = board.begin() if board is not None else None
     if attach_fn is None:
         attach_fn = lambda s: None  # noqa: E731
-    if slot is not None:
-        attach_fn(slot)
     bound = DPOW_NO_HIT
     secret = None
     k = k_start
     batches = 0
+    attached = False
     try:
+        # A rank that cannot attach its slot (e.g. the shared page refused by its GPU) fails its
+        # first batch: it stops the slot, so the other ranks' searches end at once, and votes
+        # healthy = 0 at the first boundary, so nobody waits out the vote's timeout.
+        attach_err = None
+        if slot is not None:
+            try:
+                attach_fn(slot)
+                attached = True
+            except Exception as e:
+                attach_err = e
+                board.stop(slot)
         while k < k_limit:
             ke = min(k_limit, k + batch_k)
             batch_k = min(batch_k * growth, max(batch_k, batch_k_max))
-            err = None
+            err = attach_err
+            r = None
             try:
-                r = search_fn(nonce, num_trailing_zeros, wb, wbits, k, ke, bound)
+                if err is None:
+                    r = search_fn(nonce, num_trailing_zeros, wb, wbits, k, ke, bound)
             except Exception as e:  # voted below; re-raised after the all-reduce
                 err, r = e, None
                 if slot is not None:
@@ -377,7 +400,11 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
         return NodeResult(EXHAUSTED, batches=batches)
     finally:
         if slot is not None:
-            attach_fn(None)
+            if attached:
+                try:
+                    attach_fn(None)
+                except Exception:  # never hides the error that brought us here
+                    pass
             board.end()
 
 

@@ -175,6 +175,11 @@ struct SearchWait {
     const uint64_t *early = nullptr;
     uint64_t early_seen = DPOW_NO_HIT;
     uint64_t own_posted = DPOW_NO_HIT;  // the lowest hit of ours posted early: the slot's best, not a bound
+    // Every candidate of this window below `covered` has been searched without a hit: the
+    // g_end of the last consumed launch (round 5).  Once an injected bound (another rank's
+    // hit, dpow_search_bound) is at or below it, the search is over -- the launches still in
+    // flight hold nothing below the bound -- and it returns without waiting for their drain.
+    uint64_t covered = 0;
     const uint8_t *nonce = nullptr;
     size_t nonce_len = 0;
     uint32_t ntz = 0;
@@ -296,7 +301,8 @@ void poll_early(dpow_ctx *c, SearchWait &sw) {
 
 // Wait for the completion record of launch `seq`, until `deadline` (now_ns()
 // clock; kNoDeadline: none).  Returns 1 when the record is there, 0 at the
-// deadline, < 0 on error.  Spins in the first kSpinNs of the search (the record
+// deadline, 2 when an injected bound reached what the consumed launches cover
+// (SearchWait::covered: nothing of ours is left below it), < 0 on error.  Spins in the first kSpinNs of the search (the record
 // of a launch holding a hit is the time-to-secret path), then sleeps between
 // polls; the stream is queried now and then so a failed launch, or a stream
 // that went idle without writing the record, ends the wait with an error.
@@ -317,9 +323,12 @@ int wait_record(dpow_ctx *c, uint64_t seq, int64_t deadline, SearchWait &sw) {
             if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
         }
         if (sw.early && (!spinning || it % 8 == 0)) poll_early(c, sw);
-        if (c->node && (!spinning || it % 64 == 0)) {
-            const int rc = poll_node(c, sw);
-            if (rc < 0) return rc;
+        if (!spinning || it % 64 == 0) {
+            if (c->node) {
+                const int rc = poll_node(c, sw);
+                if (rc < 0) return rc;
+            }
+            if (c->ext_bound.load(std::memory_order_acquire) <= sw.covered) return 2;
         }
         if (spinning) {
             __builtin_ia32_pause();
@@ -364,9 +373,18 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     if (c->device >= kMaxDevices) return set_error(DPOW_EINVAL, "dpow_search: device ordinal too large");
     const ActiveSearch active(c->device);
     SearchWait sw;
-    {   // spin while the first hit is expected (memoryless: from any start), 2x, within [kSpinNs, kSpinMaxNs]
-        const double expect_ns = (double)expected_first_hit(ntz, remainder_bits(worker_bits)) / kEstRate * 1e9;
-        sw.spin_ns = (int64_t)std::min<double>(std::max<double>(2.0 * expect_ns, (double)kSpinNs), (double)kSpinMaxNs);
+    {   // Spin while the first hit is expected (memoryless: from any start), 2x, within [kSpinNs,
+        // kSpinMaxNs].  The expected time is at this search's share of the device (the searches
+        // in flight on it).  A search whose hit is not expected within a few spin windows (the
+        // sweep, N >= 9, N = 8 on one GPU) spins kSpinNs only: busy-spinning a host core for
+        // 4 ms of a long search buys nothing.
+        const double searches = (double)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
+        const double expect_ns =
+            (double)expected_first_hit(ntz, remainder_bits(worker_bits)) / kEstRate * 1e9 * searches;
+        sw.spin_ns = expect_ns > 2.0 * (double)kSpinMaxNs
+                         ? kSpinNs
+                         : (int64_t)std::min<double>(std::max<double>(2.0 * expect_ns, (double)kSpinNs),
+                                                     (double)kSpinMaxNs);
     }
 
     {   // keep the stale mark within 2^30 launches of the present (int32 distance in the watcher)
@@ -381,6 +399,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     const uint64_t node_best = c->node ? __atomic_load_n(&c->node->best, __ATOMIC_ACQUIRE) : DPOW_NO_HIT;
     sw.node_seen = node_best;
     const uint64_t seq0 = c->seq;
+    sw.covered = k_begin << 8;  // nothing of this window is searched yet
     for (int64_t &t : c->diag_t) t = -1;
     if (c->node) {  // the early Found fan-out: this search's control block's early-hit word
         uint64_t *ew = reinterpret_cast<uint64_t *>(c->h_cancel + kEarlyWord) + c->ctrl_idx;
@@ -480,6 +499,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         const uint64_t seq = seq0 + lj;
         const int rc = wait_record(c, seq, kNoDeadline, sw);
         if (rc < 0) return rc;
+        if (rc == 2) return DPOW_BOUNDED;  // the launch stays in flight; marked stale on return
         LaunchSlot &slot = c->slots[seq % kRing];
         const Snap &sn = c->h_snap[seq % kRing];
         slot.in_flight = false;
@@ -510,6 +530,8 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         }
         if (sn.stop != 0u || sw.node_stop || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u)
             return DPOW_CANCELLED;
+        sw.covered = slot.g_end;
+        if (c->ext_bound.load(std::memory_order_acquire) <= sw.covered) return DPOW_BOUNDED;
         return DPOW_EXHAUSTED;
     };
     while (status == DPOW_EXHAUSTED && have) {
@@ -530,6 +552,10 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
             const size_t lj = consumed;
             const int w = wait_record(c, seq0 + lj, busy_until - kQueueLeadNs, sw);
             if (w < 0) return w;
+            if (w == 2) {
+                status = DPOW_BOUNDED;
+                continue;
+            }
             if (w == 1) {
                 const int r = consume(lj);
                 if (r < 0) return r;
@@ -929,27 +955,39 @@ int dpow_diag_node_post_at(dpow_node_slot *slot, uint64_t global_idx, int64_t t_
                     __builtin_ia32_pause();
                     continue;
                 }
-                std::vector<std::pair<int64_t, std::pair<dpow_node_slot *, uint64_t>>> work;
+                // The earliest request first (a request queued mid-batch with an
+                // earlier time waited for the whole batch before): take it, and while waiting
+                // for its time go back to the queue whenever another request arrives.
+                std::pair<int64_t, std::pair<dpow_node_slot *, uint64_t>> w;
+                int rest = 0;  // requests left in the queue when w was taken
                 {
                     std::lock_guard<std::mutex> g2(P->mu);
-                    work.swap(P->q);
-                    P->pending.fetch_sub((int)work.size(), std::memory_order_acq_rel);
+                    auto it = std::min_element(P->q.begin(), P->q.end(),
+                                               [](const auto &x, const auto &y) { return x.first < y.first; });
+                    w = *it;
+                    P->q.erase(it);
+                    rest = P->pending.fetch_sub(1, std::memory_order_acq_rel) - 1;
                 }
-                std::sort(work.begin(), work.end(),
-                          [](const auto &x, const auto &y) { return x.first < y.first; });
-                for (const auto &w : work) {
-                    for (;;) {
-                        const int64_t left = w.first - mono();
-                        if (left <= 0) break;
-                        if (left > 100000) {
-                            const struct timespec d = {0, (long)(left - 50000)};
-                            nanosleep(&d, nullptr);
-                        } else {
-                            __builtin_ia32_pause();
-                        }
+                bool requeued = false;
+                for (;;) {
+                    const int64_t left = w.first - mono();
+                    if (left <= 0) break;
+                    if (P->pending.load(std::memory_order_acquire) > rest) {  // a new one: maybe earlier
+                        std::lock_guard<std::mutex> g2(P->mu);
+                        P->q.push_back(w);
+                        P->pending.fetch_add(1, std::memory_order_release);
+                        requeued = true;
+                        break;
                     }
-                    dpow_node_post(w.second.first, w.second.second);
+                    if (left > 100000) {
+                        const struct timespec d = {0, (long)std::min<int64_t>(left - 50000, 50000)};
+                        nanosleep(&d, nullptr);
+                    } else {
+                        __builtin_ia32_pause();
+                    }
                 }
+                if (requeued) continue;
+                dpow_node_post(w.second.first, w.second.second);
                 idle_since = mono();
             }
         }).detach();

@@ -3,12 +3,15 @@
 
 Rank r of G = 2^b owns the reference worker partition (WorkerByte = r,
 WorkerBits = b): threadBytes [r * 2^(8-b), (r+1) * 2^(8-b)) (worker.go:302-316).
-All ranks scan the same k-window per batch.  At each batch boundary one
-all-reduce MIN over [best global index, -running] (16 bytes; torch.distributed,
-i.e. RCCL over xGMI with the "nccl" backend) picks the globally lowest index and
-votes on cancellation.  The minimum over partitions of each partition's first
-hit is the workerBits = 0 answer, so the result is deterministic and equals the
-single-worker enumeration's first hit.
+All ranks scan the same k-window per batch.  At each batch boundary the ranks take
+one MIN of three int64 values, [best global index, running, healthy] (24 bytes): it
+picks the globally lowest index and votes on cancellation and on failure.  When every
+rank shares one host the MIN goes through the node board's shared memory
+(NodeBoard.vote, dpow_node_vote: a few microseconds); across hosts it is one
+torch.distributed all-reduce, RCCL over xGMI with the "nccl" backend (bench.py's
+per-step reduce of the sweep is RCCL too).  The minimum over partitions of each
+partition's first hit is the workerBits = 0 answer, so the result is deterministic and
+equals the single-worker enumeration's first hit.
 
 This replaces the reference's first-message-wins gather (coordinator.go:202) by
 a deterministic reduction; the owner of the winning index is rank
@@ -237,7 +240,15 @@ class NodeBoard:
     def close(self):
         """Unmap the board (every rank's context detached first: node_mine detaches at its
         end); the library drops its HIP registration of the pages (dpow_node_release), so a
-        later board mapped at the same address is registered afresh."""
+        later board mapped at the same address is registered afresh.  A local() board
+        releases its pages the same way before its memory goes (dpow.h: mandatory for any
+        slot memory)."""
+        if self._shm is None and self._base:
+            from ._lib import check, lib
+            check(lib().dpow_node_release(self._base, self.nbytes(self.world)), "dpow_node_release")
+            self._base = 0
+            self._mem = None
+            return
         if self._shm is not None:
             from ._lib import DpowError, check, lib
             err = None

@@ -141,10 +141,14 @@ typedef struct dpow_node_slot {
  * per process and stays registered while any context that attached it is open, so
  * detaching and re-attaching costs nothing and several contexts may share a slot. */
 int dpow_node_attach(dpow_ctx *ctx, dpow_node_slot *slot);
-/* Memory holding slots is about to be unmapped: waits for the launches of every
+/* Memory holding slots is about to be unmapped or freed: waits for the launches of every
  * context that attached a slot in [mem, mem + len), then drops the library's HIP
  * registration of those pages (so a later mapping at the same address is registered
- * afresh).  DPOW_EINVAL if a context is still attached to a slot there (ABI 3). */
+ * afresh).  DPOW_EINVAL if a context is still attached to a slot there (ABI 3).
+ * Mandatory before any memory that held an attached slot is unmapped or freed, whoever
+ * owns it (a shared mapping, a heap buffer, a Go or Python array): the library keys its
+ * registrations on the page address, so a later slot at the same address would otherwise
+ * be matched to the old registration and its stale device alias. */
 int dpow_node_release(void *mem, size_t len);
 /* best = DPOW_NO_HIT, stop = 0 (before the node's search that uses the slot). */
 void dpow_node_slot_reset(dpow_node_slot *slot);

@@ -64,7 +64,7 @@ def test_too_few_gpus_is_an_error():
 def test_failing_ranks_fail_the_bench():
     """The child's exit code is bench.py's: here both ranks fail (no GPU in this container)
     and bench.py exits non-zero with no result line (on the GPU box the same command is
-    the 2-rank gloo rehearsal, tools/gpu_check.sh)."""
+    the 2-rank gloo rehearsal, tools/gpu.sh check)."""
     import torch
     if torch.cuda.is_available():
         import pytest

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-search launch table of a rocprofv3 kernel trace of tools/concurrent_rate.py
-(tools/gpu_conc_trace.sh): for each stream (one search), its md5 launches, their grids and
+(rocprofv3 --kernel-trace of tools/concurrent_rate.py): for each stream (one search), its md5 launches, their grids and
 median length, and the trace's span.
     python3 tools/conc_trace_table.py gpurun_out/<tag>/w8/kt_kernel_trace.csv"""
 import collections

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Table of tools/gpu_node_ab.sh results: node ms / owner ms per G8 case and variant.
+"""Table of `tools/gpu.sh node-ab` results: node ms / owner ms per G8 case and variant.
     python3 tools/node_ab_table.py gpurun_out/<tag>"""
 import glob
 import json

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Launch timeline of single-GPU time-to-secret from a rocprofv3 kernel trace of
-tools/tts_trace.py (tools/gpu_check.sh runs both):
+tools/tts_trace.py (`tools/gpu.sh check` runs both):
 
     python3 tools/tts_timeline.py gpurun_out/<tag>/tts/trace/run_kernel_trace.csv \
         gpurun_out/<tag>/tts/tts.json > profiles/<round>_tts_timeline.json

@@ -5,7 +5,9 @@ drains after the owner's posted hit (tools/node_probe.py emulates the node the s
 
     make -C distributed-proof-of-work_amd/csrc BUILD=build_trace OUT=../distpow/libdpow_trace.so \
         EXTRA=-DDPOW_WAVE_TRACE=1 ../distpow/libdpow_trace.so
-    DPOW_LIB_PATH=distributed-proof-of-work_amd/distpow/libdpow_trace.so python3 tools/wave_trace_node.py
+    DPOW_LIB_PATH=distributed-proof-of-work_amd/distpow/libdpow_trace.so python3 tools/wave_trace_node.py [G,...] [nonce/N,...]
+
+G = 1 traces one GPU's Miner.mine (bench.py's N = 1 time-to-secret) instead of a node rank.
 
 For every case it runs the owner alone (node_mine over a local board, as node_probe.py), then
 one non-owner with the owner's hit posted at the owner's post time, and reads the per-wave
@@ -28,7 +30,8 @@ from distpow import _lib  # noqa: E402
 from distpow.node import NodeBoard, node_mine, owner_rank  # noqa: E402
 
 W, F = 8192, 8
-CASES = [([2, 2, 2, 2], 8, 293615578), ([1, 2, 3, 4], 7, 231910082), ([1, 2, 3, 4], 6, 2532284)]
+CASES = [([2, 2, 2, 2], 8, 293615578), ([1, 2, 3, 4], 7, 231910082), ([1, 2, 3, 4], 6, 2532284),
+         ([5, 6, 7, 8], 5, 167625), ([2, 2, 2, 2], 5, None)]
 
 
 def read(fn):
@@ -97,7 +100,12 @@ def main():
     lib = distpow.lib()
     board = NodeBoard.local()
     out = {"build_id": distpow.build_id(), "cases": {}}
-    G = 8
+    gs = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [8]
+    want = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "pow_golden.json")))
+    exp = {(tuple(e["nonce"]), e["ntz"]): e["global_idx"] for e in gold["first_hits"]}
+    cases = [(nc, n, exp[(tuple(nc), n)]) for nc, n, _ in CASES
+             if want is None or f"{bytes(nc).hex()}/{n}" in want]
     with distpow.Miner(0) as m:
         m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 26))  # warm
         found_at = {}
@@ -114,7 +122,7 @@ def main():
 
         warm = NodeBoard.local()
 
-        def run(nonce, n, rank, post_ns=None, g=None):
+        def run(nonce, n, rank, post_ns=None, g=None, G=8):
             slot = board.begin()
             lib.dpow_diag_node_post_at(warm.slot(0), 0, 0)  # the poster thread running before the clock
             torch.cuda.synchronize()
@@ -123,22 +131,28 @@ def main():
             t0 = time.perf_counter_ns()
             if post_ns is not None:
                 lib.dpow_diag_node_post_at(slot, g, t0 + post_ns)
-            res = node_mine(search, nonce, n, rank, G, board=board, attach_fn=m.attach_node)
+            if G == 1:
+                res = m.mine(nonce, n)
+            else:
+                res = node_mine(search, nonce, n, rank, G, board=board, attach_fn=m.attach_node)
             dt = time.perf_counter_ns() - t0
             torch.cuda.synchronize()
             after = [read(f) for f in fns]
             return res, dt, found_at.get("t", t0 + dt) - t0, summarize(before, after)
 
-        for nonce, n, g in CASES:
-            o = owner_rank(g, G)
+        for G, (nonce, n, g) in [(G, c) for G in gs for c in cases]:
+            o = owner_rank(g, G) if G > 1 else 0
             non = (o + 1) % G
+            key = f"G{G} {bytes(nonce).hex()}/{n}"
             for rep in range(3):
-                res, dt, tp, tr = run(nonce, n, o)
+                res, dt, tp, tr = run(nonce, n, o, G=G)
                 assert res.global_idx == g
-                key = f"{bytes(nonce).hex()}/{n}"
                 out["cases"].setdefault(key, []).append({"role": "owner", "rank": o, "ms": round(dt / 1e6, 3),
                                                          "post_ms": round(tp / 1e6, 3), "trace": tr})
-                res2, dt2, _, tr2 = run(nonce, n, non, post_ns=tp, g=g)
+                if G == 1:
+                    print(f"{key} rep {rep}: {dt / 1e6:.3f} ms", file=sys.stderr, flush=True)
+                    continue
+                res2, dt2, _, tr2 = run(nonce, n, non, post_ns=tp, g=g, G=G)
                 out["cases"][key].append({"role": "non-owner", "rank": non, "ms": round(dt2 / 1e6, 3),
                                           "post_ms": round(tp / 1e6, 3), "trace": tr2})
                 print(f"{key} rep {rep}: owner {dt / 1e6:.3f} ms (post {tp / 1e6:.3f}), non-owner {dt2 / 1e6:.3f} ms",

@@ -137,6 +137,9 @@ constexpr int64_t kEstFixedNs = 8000;
 // every search's grid follows the others that start or end beside it.
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_active[kMaxDevices];
+// Contexts open per device in this process: more than one means other searches may start
+// beside this one at any moment (a worker pool, the coordinator mirror's logical workers).
+std::atomic<int> g_open[kMaxDevices];
 
 struct ActiveSearch {
     int dev;
@@ -202,6 +205,7 @@ struct SearchWait {
 
 struct dpow_ctx {
     int device = 0;
+    bool counted = false;  // in g_open
     hipStream_t stream = nullptr;
     Ctrl *d_ctrl = nullptr;  // kCtrlRing control blocks (kCtrlStride apart, aligned to the ring's size);
                              //  ctrl_idx's is clean
@@ -574,7 +578,15 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         Launch &L = pl.L;
         // This search's share of the device's resident workgroups (searches sharing the device:
         // plan.h grid_share, cap_shared_launch).
-        const uint64_t active = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
+        uint64_t active = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
+        if (active == 1 && now_ns() - sw.t0 < kYoungNs) {
+            // A young search that looks alone while other contexts of this process are open on
+            // the device plans as if they all searched: its first long launch no longer takes
+            // the whole device for its full length just because it registered first (round 4:
+            // one 16-28 ms full-device launch, config 4's one nonce 8.5-23 ms over runs).
+            const int open = g_open[c->device].load(std::memory_order_relaxed);
+            if (open > 1) active = (uint64_t)open;
+        }
         const uint64_t share = grid_share(active, c->knobs);
         cap_shared_launch(planner, pl, active, c->knobs);
         uint64_t worker_blocks = 0;
@@ -771,12 +783,17 @@ int dpow_open(int device, dpow_ctx **out) {
         dpow_close(c);
         return hip_fail(e, "dpow_open: loading the search kernels");
     }
+    if (device < kMaxDevices) {
+        g_open[device].fetch_add(1, std::memory_order_relaxed);
+        c->counted = true;
+    }
     *out = c;
     return 0;
 }
 
 void dpow_close(dpow_ctx *c) {
     if (!c) return;
+    if (c->counted) g_open[c->device].fetch_sub(1, std::memory_order_relaxed);
     const DeviceScope on_device(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     // Drained: no watcher of ours reads the node pages any more.  Leave the page registry

@@ -4,6 +4,7 @@
 #
 #   gpurun --timeout 1500 -- bash tools/gpu.sh <task> <tag> [args]
 #
+#   tests            the GPU test suite (pytest -m gpu)
 #   check            GPU tests, the driver's default bench line, the 2-rank bench through
 #                    bench.py's own launcher (gloo, both ranks on the one GPU), the time-to-secret
 #                    launch timeline under rocprofv3
@@ -52,6 +53,7 @@ rehearse() {
 }
 
 case $task in
+tests) tests ;;
 check) check ;;
 final)
     check &&

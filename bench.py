@@ -319,7 +319,7 @@ def main(argv=None, miner_factory=None, gpu=None):
                                                barrier, gpu))
         guard.update("time_to_secret_node_search",
                      "one rank: Miner.mine" if world == 1 else
-                     ("node_mine (batch-synchronous, node board)" if board is not None
+                     ("node_mine (batch-synchronous, node board; native loop dpow_node_mine)" if board is not None
                       else "node_mine (batch-synchronous)") if NODE_SYNC else
                      "node_mine_async (ticked all-reduce, bound injection)")
 
@@ -492,7 +492,7 @@ def time_to_secret(miner, rank, world, dev, board, barrier, gpu):
                     res = NodeResult(r.status, r.global_idx, r.secret, 0, 0)
                 elif NODE_SYNC:  # batch-synchronous node search, Found fan-out through the node board
                     res = node_mine(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world, device=dev,
-                                    board=board, attach_fn=miner.attach_node)
+                                    board=board, attach_fn=miner.attach_node, miner=miner)
                 else:  # no batch boundaries: ticked all-reduce + the node's best injected into each rank's search
                     res = node_mine_async(lambda *a: miner.search(*a[:6], bound=a[6]), nonce, n, rank, world,
                                           bound_fn=miner.bound, cancel_fn=miner.cancel, clear_fn=miner.clear_cancel,
@@ -667,7 +667,8 @@ def collective_probe(miner, rank, world, dev, board, backend, gpu, reps=200):
             dist.barrier()
             gpu.synchronize()
             t = time.perf_counter()
-            res = node_mine(search, nonce, n, rank, world, device=dev, board=board, attach_fn=miner.attach_node)
+            res = node_mine(search, nonce, n, rank, world, device=dev, board=board, attach_fn=miner.attach_node,
+                            miner=miner)
             ms.append((time.perf_counter() - t) * 1e3)
             if not (res.status == distpow.FOUND and res.secret is not None and distpow.verify(nonce, res.secret, n)):
                 wrong.append(f"node_mine {bytes(nonce).hex()}/{n}: status {res.status}, index {res.global_idx}")

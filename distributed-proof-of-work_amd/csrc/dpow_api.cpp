@@ -935,6 +935,78 @@ int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, u
     return 0;
 }
 
+int dpow_node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *votes, uint32_t rank, uint32_t world,
+                   uint64_t *epoch, int64_t vote_timeout_ns, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,
+                   uint64_t k_begin, uint64_t k_limit, uint64_t first_k, uint64_t batch_k, uint64_t *best_global_idx,
+                   uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len, uint32_t *batches) {
+    if (!c || !slot || !epoch || !best_global_idx || !secret_out || !secret_len || !batches)
+        return set_error(DPOW_EINVAL, "dpow_node_mine: NULL argument");
+    if (world == 0 || (world & (world - 1)) != 0 || world > 256 || rank >= world)
+        return set_error(DPOW_EINVAL, "dpow_node_mine: world must be a power of two <= 256, rank < world");
+    if (batch_k == 0 || k_limit > DPOW_K_LIMIT) return set_error(DPOW_EINVAL, "dpow_node_mine: bad window");
+    // The partition of rank r of world 2^b: worker_byte = r, worker_bits = b (coordinator.go:127,326).
+    const uint32_t wbits = (uint32_t)__builtin_ctz(world);
+    *batches = 0;
+    *secret_len = 0;
+    // A rank that cannot attach the slot fails its first batch: it stops the slot (the other
+    // ranks' searches end at once) and votes healthy = 0 at the first boundary.
+    int err = dpow_node_attach(c, slot);
+    if (err < 0) dpow_node_stop(slot);
+    uint64_t k = k_begin, window = first_k ? first_k : batch_k;
+    uint8_t sec[DPOW_MAX_SECRET];
+    size_t slen = 0;
+    uint64_t own = DPOW_NO_HIT;  // this rank's verified hit (the secret bytes are ours)
+    int status = DPOW_EXHAUSTED;
+    while (k < k_limit) {
+        const uint64_t ke = k_limit - k > window ? k + window : k_limit;
+        window = batch_k;
+        int rc = DPOW_EXHAUSTED;
+        if (err == 0) {
+            uint64_t best = DPOW_NO_HIT;
+            rc = dpow_search(c, nonce, nonce_len, ntz, rank, wbits, k, ke, &best, sec, &slen);
+            if (rc < 0) {
+                err = rc;
+                dpow_node_stop(slot);
+            } else if (rc == DPOW_FOUND && best < own) {
+                own = best;
+                memcpy(secret_out, sec, slen);
+                *secret_len = slen;
+            }
+        }
+        const int64_t running =
+            (err != 0 || rc == DPOW_CANCELLED || __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) ? 0 : 1;
+        const uint64_t posted = __atomic_load_n(&slot->best, __ATOMIC_ACQUIRE);
+        const int64_t in[3] = {(int64_t)(own < posted ? own : posted), running, err != 0 ? 0 : 1};
+        int64_t out[3] = {in[0], in[1], in[2]};
+        if (votes) {
+            const int vr = dpow_node_vote(votes, rank, world, ++*epoch, in, out, vote_timeout_ns);
+            if (vr < 0) {
+                err = err ? err : vr;
+                out[2] = 0;
+            }
+        }
+        ++*batches;
+        if (out[2] == 0) {  // a rank failed: the node's search is lost (coordinator.go:202-206)
+            status = err ? err : set_error(DPOW_EPROTO, "dpow_node_mine: another rank's search failed");
+            break;
+        }
+        if ((uint64_t)out[0] != DPOW_NO_HIT) {
+            *best_global_idx = (uint64_t)out[0];
+            if ((uint64_t)out[0] != own) dpow_secret_from_index((uint64_t)out[0], secret_out, secret_len);
+            status = DPOW_FOUND;
+            break;
+        }
+        if (out[1] == 0) {
+            status = DPOW_CANCELLED;
+            break;
+        }
+        k = ke;
+    }
+    if (c->node == slot) c->node = c->d_node = nullptr;  // detach (the pages stay held: dpow_node_attach)
+    if (status != DPOW_FOUND) *secret_len = 0;
+    return status;
+}
+
 int dpow_diag_node_post_at(dpow_node_slot *slot, uint64_t global_idx, int64_t t_ns) {
     if (!slot) return set_error(DPOW_EINVAL, "dpow_diag_node_post_at: slot is NULL");
     // One poster thread per process, spinning while requests may come (it exits after 2 s

@@ -60,7 +60,10 @@ namespace DPOW_KNS {
 #define DPOW_FOLD_ZERO 1  // fold always-zero message words to literal K (A/B switch)
 #endif
 #ifndef DPOW_WATCH_SLEEP
-#define DPOW_WATCH_SLEEP 32  // watcher poll interval, s_sleep units of 64 cycles
+#define DPOW_WATCH_SLEEP 16  // watcher poll interval, s_sleep units of 64 cycles (round 4: 32)
+#endif
+#ifndef DPOW_WATCH_BATCH
+#define DPOW_WATCH_BATCH 0  // 1: the watcher loads a poll's words together (A/B switch; see the comment below)
 #endif
 #ifndef DPOW_STEAL
 #define DPOW_STEAL 1  // a wave whose counter drained claims from the next counter (A/B switch)
@@ -777,8 +780,22 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 // watcher workgroup is dispatched first, and the kernel time in the completion record
 // replaces per-launch HIP timing events, whose profiling packets cost the host ~4.5 us per
 // launch on the time-to-secret path (tools/small_search_probe.py, DPOW_DIAG_NO_EVENTS).
+#ifndef DPOW_WATCH_PAD
+#define DPOW_WATCH_PAD 0
+#endif
+#ifndef DPOW_WATCH_NOINLINE
+#define DPOW_WATCH_NOINLINE 0
+#endif
+#if DPOW_WATCH_NOINLINE
+__device__ __attribute__((noinline)) void watcher(const Launch &L) {
+#else
 DPOW_DEV void watcher(const Launch &L) {
+#endif
     if (threadIdx.x != 0) return;
+#if DPOW_WATCH_PAD > 0
+    // Code-placement padding (A/B: the hash loop's start alignment follows the code before it)
+    asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(DPOW_WATCH_PAD));
+#endif
     __hip_atomic_store(&L.claim[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long node_seen = ~0ull, bound_seen = L.bound0, early_seen = kNoHit;
 #if DPOW_WAVE_TRACE
@@ -788,6 +805,62 @@ DPOW_DEV void watcher(const Launch &L) {
     wt[0] = __builtin_amdgcn_s_memrealtime();
     wt[1] = wt[2] = 0;
 #endif
+#if DPOW_WATCH_BATCH
+    // Every word of a poll is loaded at once, and the loop waits for them together: one round
+    // trip to the host's pinned pages per poll.  Polled one after another (the completion count
+    // and the best, then the flags and the bound, then the node's best, then its stop) a poll
+    // costs four round trips, ~5-7 us, which every relay waits for: the early hit to the host,
+    // another rank's posted hit into Ctrl::best, a cancel.  Without a node slot the node's
+    // words are read from the launch's own pinned words instead (no branch between the loads).
+    // Round 5 A/B (profiles/r05_watch_ab.json): the emulated node's N = 5 / 6 searches 10-13 us
+    // faster at G2-G8, but the same hash loop in another code placement made one GPU's
+    // [2,2,2,2]/8 1.48 -> 1.75 ms (the L = 3 rate -0.3 %, not the cause) and the sweep -0.3 %;
+    // off until that placement effect is understood.
+    const unsigned long long *const node_best_p = L.node_best ? L.node_best : L.ext_bound;
+    const uint32_t *const node_stop_p = L.node_stop ? L.node_stop : L.cancel;
+    for (;;) {
+        const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t cancel = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long nb = __hip_atomic_load(node_best_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t nstop = __hip_atomic_load(node_stop_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (done >= L.done_target) {
+#if DPOW_WAVE_TRACE
+            wt[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+            return;
+        }
+        if (L.early && b < early_seen) {
+#if DPOW_WAVE_TRACE
+            if (wt[2] == 0) wt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+            early_seen = b;
+            __hip_atomic_store(L.early, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        bool stop = cancel != 0u || (int32_t)(stale - L.seq) >= 0;
+        if (eb < bound_seen) {
+            bound_seen = eb;
+            __hip_atomic_fetch_min(&L.ctrl->best, eb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (L.node_best) {
+            if (nb < node_seen) {
+#if DPOW_WAVE_TRACE
+                if (wt[1] == 0 && nb < kNoHit) wt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+                node_seen = nb;
+                __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            stop = stop || nstop != 0u;
+        }
+        if (stop) {
+            __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
+    }
+#else
     for (;;) {
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (done >= L.done_target) {
@@ -831,6 +904,7 @@ DPOW_DEV void watcher(const Launch &L) {
         }
         __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
     }
+#endif
 }
 
 // One returning atomic per claim, by lane 0 (claim_issue); its result stays in

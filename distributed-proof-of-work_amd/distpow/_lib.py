@@ -194,6 +194,9 @@ def lib():
         "dpow_node_vote": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                           ctypes.c_int64]),
+        "dpow_node_mine": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, u64p, ctypes.c_int64,
+                                          ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64,
+                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, u8p, szp, u32p]),
         "dpow_secret_from_index": (ctypes.c_int, [ctypes.c_uint64, u8p, szp]),
         "dpow_md5": (None, [ctypes.c_char_p, ctypes.c_size_t, u8p]),
         "dpow_trailing_zero_nibbles": (ctypes.c_uint32, [ctypes.c_char_p]),

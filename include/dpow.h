@@ -29,9 +29,10 @@ extern "C" {
 /* 2: dpow_worker_result gained `error` (dpow_worker.h), DPOW_K_LIMIT = 2^55 - 1 and
  * 7-byte chunks (round 2); dpow_node_* (round 3).
  * 3 (round 4): dpow_diag_launch_geometry takes ntz (dpow_diag.h); dpow_node_release.
+ * 4 (round 5): dpow_node_mine.
  * A consumer built against another version must refuse the library before any
  * other call (distpow/_lib.py check_abi, tests/c/abi_harness.c). */
-#define DPOW_ABI_VERSION 3
+#define DPOW_ABI_VERSION 4
 
 /* "no hit" sentinel for global indices: INT64_MAX, so that signed (RCCL/gloo
  * int64 MIN) and unsigned (device atomicMin u64) reductions agree. */
@@ -174,6 +175,27 @@ typedef struct dpow_node_vote_entry {
 } dpow_node_vote_entry;
 int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, uint64_t epoch,
                    const int64_t in[3], int64_t out[3], int64_t timeout_ns);
+
+/* One node search of this rank, natively (ABI 4): distpow.node.node_mine's batch loop over a
+ * shared board, without a Python round per batch -- what a Go node scheduler would call.
+ * Rank `rank` of `world` (a power of two <= 256) searches its partition (worker_byte = rank,
+ * worker_bits = log2 world; coordinator.go:127,326) window by window from k_begin: the first
+ * window first_k chunks (0: batch_k), every later one batch_k, up to k_limit.  The context is
+ * attached to `slot` for the call (the Found fan-out, dpow_node_attach) and detached after it.
+ * Each window ends in the node vote through `votes` (dpow_node_vote, epoch advanced from
+ * *epoch, which the caller keeps across calls), a MIN of [the lower of its own hit and the
+ * slot's posted best, running, healthy]; votes = NULL takes this rank's values alone (one rank,
+ * or the one-GPU emulation of tools/node_probe.py).  Returns DPOW_FOUND with *best_global_idx =
+ * the node's first hit (the workerBits = 0 answer) and its secret (this rank's verified bytes,
+ * or dpow_secret_from_index of another rank's hit), DPOW_CANCELLED when some rank was
+ * cancelled (the context's cancel flag, the slot's stop), DPOW_EXHAUSTED at k_limit; this
+ * rank's error code when its own search failed (it stopped the slot and voted healthy = 0),
+ * DPOW_EPROTO when another rank's did or a vote timed out.  *batches = windows voted. */
+int dpow_node_mine(dpow_ctx *ctx, dpow_node_slot *slot, dpow_node_vote_entry *votes, uint32_t rank,
+                   uint32_t world, uint64_t *epoch, int64_t vote_timeout_ns, const uint8_t *nonce,
+                   size_t nonce_len, uint32_t ntz, uint64_t k_begin, uint64_t k_limit, uint64_t first_k,
+                   uint64_t batch_k, uint64_t *best_global_idx, uint8_t secret_out[DPOW_MAX_SECRET],
+                   size_t *secret_len, uint32_t *batches);
 
 /* ---------------------------------------------------------------------------
  * Host helpers (no GPU needed).

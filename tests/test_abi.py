@@ -49,7 +49,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_device_count():
     import distpow
     from distpow import _lib
-    assert distpow.lib().dpow_abi_version() == _lib.header_abi_version() == 3
+    assert distpow.lib().dpow_abi_version() == _lib.header_abi_version() == 4
     assert distpow.device_count() >= 0
 
 
@@ -90,7 +90,7 @@ def test_library_of_another_abi_is_refused(tmp_path):
 
 def test_library_missing_entry_points_is_refused(tmp_path):
     """The right version number but a missing entry point: refused too (no silent skip)."""
-    r = _load_in_child(_stub_library(tmp_path, 3, omit=("dpow_search_bound",)))
+    r = _load_in_child(_stub_library(tmp_path, 4, omit=("dpow_search_bound",)))
     assert r.returncode == 7, (r.stdout, r.stderr)
     assert "dpow_search_bound" in r.stdout
 
@@ -123,6 +123,11 @@ def test_null_arguments_are_errors_not_crashes():
     assert L.dpow_search(None, b"", 0, 1, 0, 0, 0, 1, None, None, None) == -1
     assert L.dpow_open(0, None) == -1
     assert L.dpow_get_stats(None, None) == -1
+    import ctypes
+    e, b, n = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint32(0)
+    sec, sl = (ctypes.c_uint8 * 16)(), ctypes.c_size_t()
+    assert L.dpow_node_mine(None, None, None, 0, 2, ctypes.byref(e), 0, b"\x01", 1, 3, 0, 1, 0, 1,
+                            ctypes.byref(b), sec, ctypes.byref(sl), ctypes.byref(n)) == -1
     L.dpow_close(None)  # no-op
 
 
@@ -158,7 +163,7 @@ def test_c_abi_from_plain_c(tmp_path):
     distpow.lib()  # the build-id check
     out = subprocess.check_output([_build_c_harness(tmp_path)], timeout=60).decode()
     rec = json.loads(out)
-    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 3
+    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 4
 
 
 @pytest.mark.gpu

@@ -63,6 +63,17 @@ def _rank_main(rank, world, port, cases, out_q):
         for nonce, ntz in cases:
             r = node_mine(search, nonce, ntz, rank, world, board=board, attach_fn=m.attach_node)
             res.append(("board", r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner))
+        # the native loop (dpow_node_mine, round 5): the same board, its vote in C; then with a
+        # first window of twice the per-rank expected first hit (first_window_k)
+        from distpow import DPOW_K_LIMIT
+        from distpow.node import BOARD_BATCH_CANDIDATES, _node_mine_native, first_window_k
+        for nonce, ntz in cases + [([1, 2, 3, 4], 3)]:
+            r = node_mine(None, nonce, ntz, rank, world, board=board, miner=m)
+            res.append(("native", r.status, r.global_idx, None if r.secret is None else list(r.secret), r.owner))
+            r = _node_mine_native(m, board, nonce, ntz, rank, world, 0, DPOW_K_LIMIT, BOARD_BATCH_CANDIDATES >> 7,
+                                  first_window_k(ntz, world, 2.0))
+            res.append(("native-first", r.status, r.global_idx, None if r.secret is None else list(r.secret),
+                        r.owner))
         # a cancel on one rank through the board: its search returns CANCELLED and raises
         # the slot's stop, which ends the other rank's search at once (not at a batch end)
         if rank == 0:
@@ -72,6 +83,13 @@ def _rank_main(rank, world, port, cases, out_q):
                       attach_fn=m.attach_node)
         m.clear_cancel()
         res.append(("board-cancel", r.status, r.batches, time.perf_counter() - t0))
+        # the same through the native loop
+        if rank == 1:
+            threading.Timer(0.3, m.cancel).start()
+        t0 = time.perf_counter()
+        r = node_mine(None, [1, 2, 3, 4], 32, rank, world, k_start=1 << 24, board=board, miner=m)
+        m.clear_cancel()
+        res.append(("native-cancel", r.status, r.batches, time.perf_counter() - t0))
         board.close()
         # a real cancel on the last rank: its pinned flag stops its kernel mid-launch, the
         # search returns CANCELLED and the all-reduce's running slot stops every rank
@@ -92,6 +110,7 @@ def test_node_mine_two_ranks_on_gpu(golden):
 
     want = [([1, 2, 3, 4], 6), ([1, 2, 3, 4], 8), ([2, 2, 2, 2], 8), ([5, 6, 7, 8], 5)]
     exp = {(tuple(e["nonce"]), e["ntz"]): e for e in golden["first_hits"]}
+    assert (1, 2, 3, 4, 3) in {tuple(k[0]) + (k[1],) for k in exp}
     cases = [c for c in want if (tuple(c[0]), c[1]) in exp]
     assert len(cases) == len(want)
     world = 2
@@ -126,7 +145,18 @@ def test_node_mine_two_ranks_on_gpu(golden):
             assert tag == "board" and status == 1 and g == e["global_idx"] and secret == e["secret"], \
                 (rank, nonce, ntz, g)
             assert owner == (g & 0xFF) >> 7
+        nat = [x for x in outs[rank] if x[0] in ("native", "native-first")]
+        assert len(nat) == 2 * (len(cases) + 1)
+        for (nonce, ntz), (tag, status, g, secret, owner) in zip([c for c in cases + [([1, 2, 3, 4], 3)]
+                                                                   for _ in (0, 1)], nat):
+            e = exp[(tuple(nonce), ntz)]
+            assert status == 1 and g == e["global_idx"] and secret == e["secret"], (rank, tag, nonce, ntz, g)
+            assert owner == (g & 0xFF) >> 7
         tag, status, batches, secs = outs[rank][-2]
+        # (its windows are board batches of 2^33 candidates per rank, ~40 ms each on the shared GPU:
+        # the stop ends the window in flight on both ranks, which voted the same windows)
+        assert tag == "native-cancel" and status == 2 and secs < 1.0, outs[rank][-2]
+        tag, status, batches, secs = outs[rank][-3]
         # the batch (2^37 candidates per rank, > 1 s on a shared GPU) ends at the stop
         assert tag == "board-cancel" and status == 2 and batches == 1 and secs < 1.0, outs[rank][-2]
         status, batches, secs = outs[rank][-1]
@@ -135,3 +165,4 @@ def test_node_mine_two_ranks_on_gpu(golden):
     # the ranks agree batch by batch
     assert [r[4] for r in outs[0][:n]] == [r[4] for r in outs[1][:n]]
     assert outs[0][-1][1] == outs[1][-1][1]
+    assert outs[0][-2][2] == outs[1][-2][2]

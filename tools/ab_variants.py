@@ -26,14 +26,19 @@ for t in range(3):
     dt = time.perf_counter() - t0
     st = m.stats()
     res.append({"wall_ghs": (1 << 34) / dt / 1e9, "kernel_ghs": st.candidates / (st.kernel_ms * 1e-3) / 1e9})
+# the L = 3 chunk segment (k in [2^16, 2^24)): the chunk-length-spanning ("_ls") kernels
+m.reset_stats()
+m.search([1,2,3,4], 32, 0, 0, 1 << 16, 1 << 24)
+st = m.stats()
+res[0]["l3_kernel_ghs"] = round(st.candidates / (st.kernel_ms * 1e-3) / 1e9, 2)
 tts = {}
-for nonce, n in ([1,2,3,4], 3), ([1,2,3,4], 6), ([1,2,3,4], 7), ([1,2,3,4], 8), ([2,2,2,2], 5):
+for nonce, n in ([1,2,3,4], 3), ([1,2,3,4], 6), ([1,2,3,4], 7), ([1,2,3,4], 8), ([2,2,2,2], 5), ([2,2,2,2], 8):
     ts = []
     for _ in range(5):
         t0 = time.perf_counter()
         r = m.mine(nonce, n)
         ts.append((time.perf_counter() - t0) * 1e3)
-    tts[f"{n}"] = sorted(ts)[len(ts) // 2]
+    tts[f"{bytes(nonce).hex()}/{n}"] = round(sorted(ts)[len(ts) // 2], 4)
 res[0]["tts_ms"] = tts
 print(json.dumps(res))
 """
@@ -52,7 +57,7 @@ def main():
             res = json.loads(r.stdout.strip().splitlines()[-1])
             out[l] += res
             print(rnd, l, " ".join(f"{x['kernel_ghs']:.1f}" for x in res),
-                  "tts_ms", json.dumps(res[0].get("tts_ms")), flush=True)
+                  "l3", res[0].get("l3_kernel_ghs"), "tts_ms", json.dumps(res[0].get("tts_ms")), flush=True)
     for l, rs in out.items():
         if rs:
             ks = sorted(x["kernel_ghs"] for x in rs)

@@ -13,6 +13,7 @@
 #                    `bench.py --gpus 8` (gloo, --same-device), the rocprofv3 kernel-trace and
 #                    PMC passes of the bench (tools/profile_gpu.sh)
 #   node [runs] [G,..] [small]   the emulated node alone
+#   node-small-ab name=lib.so ...   the emulated node's small cases per library (A/B of builds)
 #   timeline [G,..]  host timelines of one GPU's and the node ranks' searches (tools/owner_timeline.py)
 #   trace [G,..] [cases]   per-wave traces (diag build distpow/libdpow_trace.so, tools/wave_trace_node.py)
 #   layouts [log2 rounds lengths]   GPU tests, the layout check, the layout sweep (tools/layout_sweep.py)
@@ -64,6 +65,14 @@ final)
         > $out/bench_n8.json 2> $out/bench_n8.err &&
     bash tools/profile_gpu.sh $tag pmc > $out/profile.list 2>&1 ;;
 node) timeout -k 10 600 python3 -u tools/node_probe.py "${1:-3}" "${2:-2,4,8}" $3 > $out/node_probe.json 2> $out/node_probe.err ;;
+node-small-ab)  # the emulated 2/4/8-GPU node's small cases per library, twice, interleaved
+    for rnd in 1 2; do
+        for spec in "$@"; do
+            name=${spec%%=*}; lib=${spec#*=}
+            DPOW_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/node_probe.py 3 2,4,8 small \
+                > $out/node_${name}_$rnd.json 2> $out/node_${name}_$rnd.err || exit $?
+        done
+    done ;;
 timeline) timeout -k 10 300 python3 -u tools/owner_timeline.py "${1:-2,4,8}" > $out/owner_timeline.json 2> $out/owner_timeline.err ;;
 trace)
     DPOW_LIB_PATH=distributed-proof-of-work_amd/distpow/libdpow_trace.so timeout -k 10 300 \

@@ -42,6 +42,9 @@ from distpow.node import NodeBoard, node_mine, owner_rank  # noqa: E402
 # median in the 2- and 8-rank rehearsals (profiles/r03_bench_n2_rehearsal.json): added to the
 # slowest rank's time.  (Here node_mine runs without a process group or a shared board.)
 NODE_VOTE_MS = 0.0035
+# The rank's search through the native loop (dpow_node_mine, as bench.py runs it) unless
+# DPOW_NODE_PY=1 (round 4's Python loop over Miner.search).
+NATIVE = os.environ.get("DPOW_NODE_PY") != "1"
 
 
 def med(v):
@@ -103,8 +106,16 @@ def main():
                 # cost the rank 50-100 us; round 3 created a native thread per post, on the
                 # clock; now one queues a request for a poster already running)
                 lib.dpow_diag_node_post_at(slot, g, t0 + int(post_after_s * 1e9))
-            res = node_mine(search_timed, nonce, n, rank, G, board=board, attach_fn=m.attach_node)
-            dt = (time.perf_counter_ns() - t0) / 1e9
+            if NATIVE:  # the native loop (dpow_node_mine): one call; the post from the last search's timeline
+                res = node_mine(None, nonce, n, rank, G, board=board, miner=m)
+                dt = (time.perf_counter_ns() - t0) / 1e9
+                if res.status == distpow.FOUND and res.global_idx != distpow.DPOW_NO_HIT:
+                    lib.dpow_diag_search_times(m._ctx, tl)
+                    if tl[7] >= 0:  # errs early by the call's entry (~1 us), as search_timed's t_call
+                        found_at["t"] = t0 / 1e9 + tl[7] / 1e9
+            else:
+                res = node_mine(search_timed, nonce, n, rank, G, board=board, attach_fn=m.attach_node)
+                dt = (time.perf_counter_ns() - t0) / 1e9
             t_post = found_at.get("t", t0 / 1e9 + dt) - t0 / 1e9
             return res, dt, t_post
 

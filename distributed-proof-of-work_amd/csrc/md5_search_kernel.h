@@ -812,7 +812,7 @@ DPOW_DEV void watcher(const Launch &L) {
     // costs four round trips, ~5-7 us, which every relay waits for: the early hit to the host,
     // another rank's posted hit into Ctrl::best, a cancel.  Without a node slot the node's
     // words are read from the launch's own pinned words instead (no branch between the loads).
-    // Round 5 A/B (profiles/r05_watch_ab.json): the emulated node's N = 5 / 6 searches 10-13 us
+    // Round 5 A/B (profiles/r05_ab.json, r05e-r05j): the emulated node's N = 5 / 6 searches 10-13 us
     // faster at G2-G8, but the same hash loop in another code placement made one GPU's
     // [2,2,2,2]/8 1.48 -> 1.75 ms (the L = 3 rate -0.3 %, not the cause) and the sweep -0.3 %;
     // off until that placement effect is understood.

@@ -289,7 +289,10 @@ def main(argv=None, miner_factory=None, gpu=None):
     elapsed = time.perf_counter() - t0
     st = miner.stats()
     stream_ms = timer.elapsed_ms()
-    t = torch.tensor([elapsed], dtype=torch.float64)
+    # the MAX over ranks: on the host group when there is one (N > 1 over RCCL), else on the
+    # default group, whose tensors live on the GPU with the nccl backend
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device=dev if (host_group is None and args.backend == "nccl") else "cpu")
     if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=host_group)
     elapsed_max = float(t.item())

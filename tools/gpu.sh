@@ -28,6 +28,9 @@ task=${1:?task}; tag=${2:?tag}; shift 2
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
+# The in-tree libdpow.so must be the sources' build: it is built here, not on the box.
+DPOW_NO_AUTOBUILD=1 python3 -c 'import sys; sys.path.insert(0, "distributed-proof-of-work_amd"); import distpow; distpow.lib()' \
+    || { echo "tools/gpu.sh: libdpow.so does not match the sources (build it before the call)" >&2; exit 3; }
 
 tests() {
     timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v -s --timeout 120 --timeout-method thread > $out/pytest.log 2>&1

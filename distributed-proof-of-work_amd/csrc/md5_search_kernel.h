@@ -783,6 +783,17 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 #ifndef DPOW_WATCH_PAD
 #define DPOW_WATCH_PAD 0
 #endif
+#ifndef DPOW_PROLOGUE_PAD
+#define DPOW_PROLOGUE_PAD 0
+#endif
+#ifdef DPOW_VLS
+#define DPOW_VLS_UNIT DPOW_VLS
+#else
+#define DPOW_VLS_UNIT 0
+#endif
+#ifndef DPOW_PAD_4B
+#define DPOW_PAD_4B (DPOW_WATCH_BATCH == 3 ? 4 : 0)  // see search_body
+#endif
 #ifndef DPOW_WATCH_NOINLINE
 #define DPOW_WATCH_NOINLINE 0
 #endif
@@ -805,7 +816,7 @@ DPOW_DEV void watcher(const Launch &L) {
     wt[0] = __builtin_amdgcn_s_memrealtime();
     wt[1] = wt[2] = 0;
 #endif
-#if DPOW_WATCH_BATCH
+#if DPOW_WATCH_BATCH == 1
     // Every word of a poll is loaded at once, and the loop waits for them together: one round
     // trip to the host's pinned pages per poll.  Polled one after another (the completion count
     // and the best, then the flags and the bound, then the node's best, then its stop) a poll
@@ -860,6 +871,103 @@ DPOW_DEV void watcher(const Launch &L) {
         }
         __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
     }
+#elif DPOW_WATCH_BATCH == 2 || DPOW_WATCH_BATCH == 3
+    // Round 4's loop with the node's words loaded beside the flags (2: two round trips to
+    // host memory per poll instead of three with a node slot; 3: the completion count and
+    // the best in one round trip too).
+    const unsigned long long *const node_best_p = L.node_best ? L.node_best : L.ext_bound;
+    const uint32_t *const node_stop_p = L.node_stop ? L.node_stop : L.cancel;
+#if DPOW_WATCH_BATCH == 2
+    for (;;) {
+        const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done >= L.done_target) {
+#if DPOW_WAVE_TRACE
+            wt[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+            return;
+        }
+        if (L.early) {
+            const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b < early_seen) {
+#if DPOW_WAVE_TRACE
+                if (wt[2] == 0) wt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+                early_seen = b;
+                __hip_atomic_store(L.early, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t cancel = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long nb = __hip_atomic_load(node_best_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t nstop = __hip_atomic_load(node_stop_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        bool stop = cancel != 0u || (int32_t)(stale - L.seq) >= 0;
+        if (eb < bound_seen) {
+            bound_seen = eb;
+            __hip_atomic_fetch_min(&L.ctrl->best, eb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (L.node_best) {
+            if (nb < node_seen) {
+#if DPOW_WAVE_TRACE
+                if (wt[1] == 0 && nb < kNoHit) wt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+                node_seen = nb;
+                __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            stop = stop || nstop != 0u;
+        }
+        if (stop) {
+            __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
+    }
+#else
+    for (;;) {
+        const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done >= L.done_target) {
+#if DPOW_WAVE_TRACE
+            wt[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+            return;
+        }
+        if (L.early) {
+            if (b < early_seen) {
+#if DPOW_WAVE_TRACE
+                if (wt[2] == 0) wt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+                early_seen = b;
+                __hip_atomic_store(L.early, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t cancel = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long nb = __hip_atomic_load(node_best_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t nstop = __hip_atomic_load(node_stop_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        bool stop = cancel != 0u || (int32_t)(stale - L.seq) >= 0;
+        if (eb < bound_seen) {
+            bound_seen = eb;
+            __hip_atomic_fetch_min(&L.ctrl->best, eb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (L.node_best) {
+            if (nb < node_seen) {
+#if DPOW_WAVE_TRACE
+                if (wt[1] == 0 && nb < kNoHit) wt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+                node_seen = nb;
+                __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            stop = stop || nstop != 0u;
+        }
+        if (stop) {
+            __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
+    }
+#endif
 #else
     for (;;) {
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1054,6 +1162,20 @@ DPOW_DEV void search_body(const Launch &L) {
 #if DPOW_WAVE_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_first = 0, n_wb = 0, t_last = 0, c_last = 0, reason = 0, t_hit = 0;
+#endif
+#if DPOW_PROLOGUE_PAD > 0
+    // Code-placement padding of the worker path (A/B builds: the hash loop's placement follows
+    // the code in front of it).
+    asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(DPOW_PROLOGUE_PAD));
+#endif
+#if DPOW_PAD_4B > 0
+    // The 4-byte-nonce D-equality kernel (<1,1,0,eq>, the sweep's and N >= 8's), not the
+    // chunk-length-spanning unit: DPOW_PAD_4B s_nop in front of the worker path keep its hash
+    // and claim loops where round 4's build had them (tests/test_isa.py checks the offsets).
+    // The watcher's poll (DPOW_WATCH_BATCH) moved them by 16 bytes, and that placement alone
+    // cost the sweep 0.5 % (profiles/r05_ab.json[r05q/ab.log]).
+    if constexpr (EQ && NBLK == 1 && W0 == 1 && SH == 0 && !DPOW_VLS_UNIT)
+        asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(DPOW_PAD_4B));
 #endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t loff = lane_offset(L.rbits, lane);

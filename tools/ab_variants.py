@@ -40,6 +40,18 @@ for nonce, n in ([1,2,3,4], 3), ([1,2,3,4], 6), ([1,2,3,4], 7), ([1,2,3,4], 8), 
         ts.append((time.perf_counter() - t0) * 1e3)
     tts[f"{bytes(nonce).hex()}/{n}"] = round(sorted(ts)[len(ts) // 2], 4)
 res[0]["tts_ms"] = tts
+# fresh nonces (seeded): the mean time-to-secret at N = 7 and 8, where a single nonce's time
+# depends on where its hit falls among the launch's waves
+import random
+rng = random.Random(5150)
+for n, count in ((7, 16), (8, 8)):
+    ts = []
+    for _ in range(count):
+        nonce = [rng.randrange(256) for _ in range(4)]
+        t0 = time.perf_counter()
+        m.mine(nonce, n)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    res[0][f"fresh_n{n}_mean_ms"] = round(sum(ts) / len(ts), 3)
 print(json.dumps(res))
 """
 
@@ -57,7 +69,8 @@ def main():
             res = json.loads(r.stdout.strip().splitlines()[-1])
             out[l] += res
             print(rnd, l, " ".join(f"{x['kernel_ghs']:.1f}" for x in res),
-                  "l3", res[0].get("l3_kernel_ghs"), "tts_ms", json.dumps(res[0].get("tts_ms")), flush=True)
+                  "l3", res[0].get("l3_kernel_ghs"), "fresh7", res[0].get("fresh_n7_mean_ms"),
+                  "fresh8", res[0].get("fresh_n8_mean_ms"), "tts_ms", json.dumps(res[0].get("tts_ms")), flush=True)
     for l, rs in out.items():
         if rs:
             ks = sorted(x["kernel_ghs"] for x in rs)

@@ -237,6 +237,17 @@ struct dpow_ctx {
     // (launch length on a shared device), DPOW_DIAG_SHARE_MAX (grid share cap); 0 = the policy.
     LaunchKnobs knobs;
     int64_t diag_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // the last search's host timeline (dpow_diag_search_times)
+    // The last search's launches, in launch order (dpow_diag_search_launches): host times of
+    // each queueing and record consumption (absolute now_ns), the search's start.
+    struct DiagLaunch {
+        uint64_t seq = 0, candidates = 0, g_end = 0;
+        int32_t kind = 0;  // 0: the k = 0 kernel, 1: an md5 launch
+        int64_t queued = -1, seen = -1;
+    };
+    static constexpr size_t kDiagLaunches = 32;
+    DiagLaunch diag_l[kDiagLaunches];
+    size_t diag_nl = 0;
+    int64_t diag_t0 = 0;
 };
 
 namespace {
@@ -405,6 +416,13 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
     const uint64_t seq0 = c->seq;
     sw.covered = k_begin << 8;  // nothing of this window is searched yet
     for (int64_t &t : c->diag_t) t = -1;
+    c->diag_nl = 0;
+    c->diag_t0 = sw.t0;
+    auto diag_queued = [c](size_t li, uint64_t seq, int32_t kind, uint64_t cands, uint64_t g_end) {
+        if (li >= dpow_ctx::kDiagLaunches) return;
+        c->diag_l[li] = {seq, cands, g_end, kind, now_ns(), -1};
+        c->diag_nl = li + 1;
+    };
     if (c->node) {  // the early Found fan-out: this search's control block's early-hit word
         uint64_t *ew = reinterpret_cast<uint64_t *>(c->h_cancel + kEarlyWord) + c->ctrl_idx;
         __atomic_store_n(ew, (uint64_t)DPOW_NO_HIT, __ATOMIC_RELEASE);
@@ -443,6 +461,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         e = search_k0(k0, c->stream);
         if (e != hipSuccess) return hip_fail(e, "search_k0");
         c->diag_t[0] = now_ns() - sw.t0;
+        diag_queued(0, seq0, 0, k0.r, 1ull << 8);
         k0slot.in_flight = true;
         k0slot.seq = seq0;
         k0slot.candidates = k0.r;
@@ -512,6 +531,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         if (sn.t_start != 0ull && sn.t_end >= sn.t_start)
             c->stats.kernel_ms += (double)(sn.t_end - sn.t_start) * kRealtimeNs * 1e-6;
         if (consumed == 0) c->diag_t[2] = now_ns() - sw.t0;
+        if (lj < dpow_ctx::kDiagLaunches) c->diag_l[lj].seen = now_ns();
         consumed = lj + 1;
         // The watcher may have put the node slot's best into Ctrl::best before this thread
         // saw it: read the slot now (its best only decreases) so ext_bound covers it.
@@ -610,6 +630,7 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
                           c->stream);
         if (e != hipSuccess) return hip_fail(e, "search_launch");
         if (!md5_queued) c->diag_t[1] = now_ns() - sw.t0;
+        diag_queued(li, seq, 1, L.i_end - L.i_begin, pl.info.k_end << 8);
         md5_queued = true;
         slot.seq = seq;
         slot.in_flight = true;
@@ -1185,6 +1206,74 @@ int dpow_diag_search_times(dpow_ctx *c, int64_t out[8]) {
     if (!c || !out) return set_error(DPOW_EINVAL, "dpow_diag_search_times: NULL argument");
     for (int i = 0; i < 8; ++i) out[i] = c->diag_t[i];
     return 0;
+}
+
+int dpow_diag_search_launches(dpow_ctx *c, int64_t *t0_ns, dpow_diag_launch_time *out, size_t max_launches) {
+    if (!c || !t0_ns) return set_error(DPOW_EINVAL, "dpow_diag_search_launches: NULL argument");
+    *t0_ns = c->diag_t0;
+    const size_t n = c->diag_nl;
+    for (size_t i = 0; out && i < n && i < max_launches; ++i) {
+        const dpow_ctx::DiagLaunch &d = c->diag_l[i];
+        dpow_diag_launch_time &o = out[i];
+        o.seq = d.seq;
+        o.kind = d.kind;
+        o.queued_ns = d.queued;
+        o.seen_ns = d.seen;
+        o.candidates = d.candidates;
+        o.g_end = d.g_end;
+        const Snap &sn = c->h_snap[d.seq % kRing];
+        const bool rec = __atomic_load_n(&sn.seq, __ATOMIC_ACQUIRE) == (uint32_t)(d.seq + 1);
+        o.recorded = rec ? 1 : 0;
+        o.t_start_tick = rec ? sn.t_start : 0;
+        o.t_end_tick = rec ? sn.t_end : 0;
+        o.best = rec ? sn.best : DPOW_NO_HIT;
+    }
+    return (int)n;
+}
+
+int dpow_diag_clock_sync(dpow_ctx *c, int reps, int64_t *offset_ns) {
+    if (!c || !offset_ns || reps < 1) return set_error(DPOW_EINVAL, "dpow_diag_clock_sync: bad argument");
+    const DeviceScope on_device(c->device);
+    if (on_device.e != hipSuccess) return hip_fail(on_device.e, "hipSetDevice");
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(e, "dpow_diag_clock_sync: hipStreamSynchronize");
+    unsigned long long *h = nullptr, *d = nullptr;
+    if ((e = hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
+        return hip_fail(e, "dpow_diag_clock_sync: hipHostMalloc");
+    if ((e = hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0)) != hipSuccess) {
+        (void)hipHostFree(h);
+        return hip_fail(e, "dpow_diag_clock_sync: hipHostGetDevicePointer");
+    }
+    int64_t best = INT64_MAX;
+    int rc = 0;
+    for (int r = 0; r < reps && rc == 0; ++r) {
+        __atomic_store_n(h, 0ull, __ATOMIC_RELEASE);
+        if ((e = clock_probe(d, c->stream)) != hipSuccess) {
+            rc = hip_fail(e, "dpow_diag_clock_sync: clock_probe");
+            break;
+        }
+        const int64_t t_launch = now_ns();
+        unsigned long long tick = 0;
+        int64_t t = 0;
+        while ((tick = __atomic_load_n(h, __ATOMIC_ACQUIRE)) == 0ull) {
+            t = now_ns();
+            if (t - t_launch > 1000000000) {
+                rc = set_error(DPOW_EHIP, "dpow_diag_clock_sync: the probe's stamp never arrived");
+                break;
+            }
+            __builtin_ia32_pause();
+        }
+        if (rc) break;
+        t = now_ns();
+        // The stamp reached host memory at or before t: the least delayed pairing bounds the offset.
+        const int64_t off = t - (int64_t)((double)tick * kRealtimeNs);
+        if (off < best) best = off;
+    }
+    e = hipStreamSynchronize(c->stream);
+    if (rc == 0 && e != hipSuccess) rc = hip_fail(e, "dpow_diag_clock_sync: hipStreamSynchronize");
+    (void)hipHostFree(h);
+    if (rc == 0) *offset_ns = best;
+    return rc;
 }
 
 uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t worker_bits) {

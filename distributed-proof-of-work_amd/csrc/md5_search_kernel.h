@@ -63,7 +63,10 @@ namespace DPOW_KNS {
 #define DPOW_WATCH_SLEEP 16  // watcher poll interval, s_sleep units of 64 cycles (round 4: 32)
 #endif
 #ifndef DPOW_WATCH_BATCH
-#define DPOW_WATCH_BATCH 0  // 1: the watcher loads a poll's words together (A/B switch; see the comment below)
+#define DPOW_WATCH_BATCH 1  // the watcher loads a poll's words together (0: round 4's poll; A/B switch)
+#endif
+#ifndef DPOW_HIT_EARLY
+#define DPOW_HIT_EARLY 0  // 1: a wave's hit goes to the early-hit word from the hit path (A/B switch)
 #endif
 #ifndef DPOW_STEAL
 #define DPOW_STEAL 1  // a wave whose counter drained claims from the next counter (A/B switch)
@@ -752,6 +755,9 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
     __hip_atomic_store(&snap->t_start, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&snap->t_end, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&snap->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#if DPOW_WAVE_TRACE
+    g_wave_trace[kTraceFields * (kTraceWaves - 2) + 3] = __builtin_amdgcn_s_memrealtime();  // the record released
+#endif
 }
 
 // Workgroup 0, one lane: relays the host cancel flag to Ctrl::stop while the
@@ -792,7 +798,7 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 #define DPOW_VLS_UNIT 0
 #endif
 #ifndef DPOW_PAD_4B
-#define DPOW_PAD_4B (DPOW_WATCH_BATCH == 3 ? 4 : 0)  // see search_body
+#define DPOW_PAD_4B (DPOW_WATCH_BATCH ? 63 : 0)  // see search_body
 #endif
 #ifndef DPOW_WATCH_NOINLINE
 #define DPOW_WATCH_NOINLINE 0
@@ -816,27 +822,26 @@ DPOW_DEV void watcher(const Launch &L) {
     wt[0] = __builtin_amdgcn_s_memrealtime();
     wt[1] = wt[2] = 0;
 #endif
-#if DPOW_WATCH_BATCH == 1
-    // Every word of a poll is loaded at once, and the loop waits for them together: one round
-    // trip to the host's pinned pages per poll.  Polled one after another (the completion count
-    // and the best, then the flags and the bound, then the node's best, then its stop) a poll
-    // costs four round trips, ~5-7 us, which every relay waits for: the early hit to the host,
-    // another rank's posted hit into Ctrl::best, a cancel.  Without a node slot the node's
-    // words are read from the launch's own pinned words instead (no branch between the loads).
-    // Round 5 A/B (profiles/r05_ab.json, r05e-r05j): the emulated node's N = 5 / 6 searches 10-13 us
-    // faster at G2-G8, but the same hash loop in another code placement made one GPU's
-    // [2,2,2,2]/8 1.48 -> 1.75 ms (the L = 3 rate -0.3 %, not the cause) and the sweep -0.3 %;
-    // off until that placement effect is understood.
-    const unsigned long long *const node_best_p = L.node_best ? L.node_best : L.ext_bound;
-    const uint32_t *const node_stop_p = L.node_stop ? L.node_stop : L.cancel;
+#if DPOW_WATCH_BATCH
+    // Every word of a poll is loaded at once and waited for together: one round trip to the
+    // host's pinned pages per poll.  Round 4's loop (DPOW_WATCH_BATCH 0, below) consumed each
+    // load before issuing the next -- the completion count, the best, then the flags, the bound
+    // and the node's words: four round trips, ~8 us per poll under load
+    // (tools/search_timeline.py, profiles/r05_ab.json[r05s/]), which every relay waited for:
+    // an owner's hit to its early-hit word, another rank's posted hit into Ctrl::best, the
+    // watcher's own exit behind the last workgroup (the next launch's start).  The node slot's
+    // words are read through pointers selected inside the loop (without a slot: the launch's
+    // own bound and cancel words), so the selection stays out of the kernel's entry block.
     for (;;) {
+        const unsigned long long *const nbp = L.node_best ? L.node_best : L.ext_bound;
+        const uint32_t *const nsp = L.node_stop ? L.node_stop : L.cancel;
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t cancel = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const unsigned long long nb = __hip_atomic_load(node_best_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t nstop = __hip_atomic_load(node_stop_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long nb = __hip_atomic_load(nbp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t nstop = __hip_atomic_load(nsp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (done >= L.done_target) {
 #if DPOW_WAVE_TRACE
             wt[3] = __builtin_amdgcn_s_memrealtime();
@@ -871,103 +876,6 @@ DPOW_DEV void watcher(const Launch &L) {
         }
         __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
     }
-#elif DPOW_WATCH_BATCH == 2 || DPOW_WATCH_BATCH == 3
-    // Round 4's loop with the node's words loaded beside the flags (2: two round trips to
-    // host memory per poll instead of three with a node slot; 3: the completion count and
-    // the best in one round trip too).
-    const unsigned long long *const node_best_p = L.node_best ? L.node_best : L.ext_bound;
-    const uint32_t *const node_stop_p = L.node_stop ? L.node_stop : L.cancel;
-#if DPOW_WATCH_BATCH == 2
-    for (;;) {
-        const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done >= L.done_target) {
-#if DPOW_WAVE_TRACE
-            wt[3] = __builtin_amdgcn_s_memrealtime();
-#endif
-            return;
-        }
-        if (L.early) {
-            const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (b < early_seen) {
-#if DPOW_WAVE_TRACE
-                if (wt[2] == 0) wt[2] = __builtin_amdgcn_s_memrealtime();
-#endif
-                early_seen = b;
-                __hip_atomic_store(L.early, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t cancel = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const unsigned long long nb = __hip_atomic_load(node_best_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t nstop = __hip_atomic_load(node_stop_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        bool stop = cancel != 0u || (int32_t)(stale - L.seq) >= 0;
-        if (eb < bound_seen) {
-            bound_seen = eb;
-            __hip_atomic_fetch_min(&L.ctrl->best, eb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (L.node_best) {
-            if (nb < node_seen) {
-#if DPOW_WAVE_TRACE
-                if (wt[1] == 0 && nb < kNoHit) wt[1] = __builtin_amdgcn_s_memrealtime();
-#endif
-                node_seen = nb;
-                __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            stop = stop || nstop != 0u;
-        }
-        if (stop) {
-            __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
-    }
-#else
-    for (;;) {
-        const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done >= L.done_target) {
-#if DPOW_WAVE_TRACE
-            wt[3] = __builtin_amdgcn_s_memrealtime();
-#endif
-            return;
-        }
-        if (L.early) {
-            if (b < early_seen) {
-#if DPOW_WAVE_TRACE
-                if (wt[2] == 0) wt[2] = __builtin_amdgcn_s_memrealtime();
-#endif
-                early_seen = b;
-                __hip_atomic_store(L.early, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t cancel = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const unsigned long long nb = __hip_atomic_load(node_best_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t nstop = __hip_atomic_load(node_stop_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        bool stop = cancel != 0u || (int32_t)(stale - L.seq) >= 0;
-        if (eb < bound_seen) {
-            bound_seen = eb;
-            __hip_atomic_fetch_min(&L.ctrl->best, eb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (L.node_best) {
-            if (nb < node_seen) {
-#if DPOW_WAVE_TRACE
-                if (wt[1] == 0 && nb < kNoHit) wt[1] = __builtin_amdgcn_s_memrealtime();
-#endif
-                node_seen = nb;
-                __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            stop = stop || nstop != 0u;
-        }
-        if (stop) {
-            __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
-    }
-#endif
 #else
     for (;;) {
         const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1113,6 +1021,13 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
                     const unsigned long long prev = __hip_atomic_fetch_min(
                         &L.ctrl->best, (unsigned long long)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("; dpow: atomicMin performed (%0)" ::"v"(prev));
+#if DPOW_HIT_EARLY
+                    // With a node slot attached, a hit that lowered Ctrl::best goes to the pinned
+                    // early-hit word at once (the host verifies and posts it to the node), not at
+                    // the watcher's next poll.
+                    if (L.early != nullptr && prev > (unsigned long long)g)
+                        __hip_atomic_store(L.early, (unsigned long long)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
                 }
                 return g;
             }
@@ -1170,10 +1085,12 @@ DPOW_DEV void search_body(const Launch &L) {
 #endif
 #if DPOW_PAD_4B > 0
     // The 4-byte-nonce D-equality kernel (<1,1,0,eq>, the sweep's and N >= 8's), not the
-    // chunk-length-spanning unit: DPOW_PAD_4B s_nop in front of the worker path keep its hash
-    // and claim loops where round 4's build had them (tests/test_isa.py checks the offsets).
-    // The watcher's poll (DPOW_WATCH_BATCH) moved them by 16 bytes, and that placement alone
-    // cost the sweep 0.5 % (profiles/r05_ab.json[r05q/ab.log]).
+    // chunk-length-spanning unit: DPOW_PAD_4B s_nop in front of the worker path put its hash
+    // block at round 4's offset modulo 256 (tests/test_isa.py checks it).  Any change to the
+    // watcher re-runs the whole kernel's register allocation (it is inlined: a noinline
+    // watcher costs the hash block 24 VALU per wave-block), and the one-round-trip poll moved
+    // the hash block by 4 bytes; a move of that kind alone cost the sweep 0.5 % in round 5
+    // (profiles/r05_ab.json[r05q/ab.log]).  Padded: 218.8 vs 218.7 GH/s ([r05s/ab.log]).
     if constexpr (EQ && NBLK == 1 && W0 == 1 && SH == 0 && !DPOW_VLS_UNIT)
         asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(DPOW_PAD_4B));
 #endif
@@ -1461,10 +1378,24 @@ DPOW_DEV void search_body(const Launch &L) {
         // claim of the workgroup is performed before its retirement count.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+#if DPOW_WAVE_TRACE
+    const unsigned long long t_claims = __builtin_amdgcn_s_memrealtime();
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) {
+#if DPOW_WAVE_TRACE
+        const unsigned long long t_bar = __builtin_amdgcn_s_memrealtime();
+#endif
         const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if DPOW_WAVE_TRACE
+        if (prev + 1u == L.done_target) {  // the publisher's retirement: slot kTraceWaves - 2
+            unsigned long long *r = g_wave_trace + kTraceFields * (kTraceWaves - 2);
+            r[0] = t_claims;
+            r[1] = t_bar;
+            r[2] = __builtin_amdgcn_s_memrealtime() + (prev & 0);
+        }
+#endif
         if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
     }
 }

@@ -59,5 +59,8 @@ hipError_t search_k0_prepare();
 // zero claim counters.
 hipError_t context_init(Ctrl *ctrl, uint32_t n_ctrl, unsigned long long *claims, uint32_t n_claims,
                         hipStream_t stream);
+// One thread stamps s_memrealtime into *out (system scope): the host/device clock pairing of
+// dpow_diag_clock_sync.
+hipError_t clock_probe(unsigned long long *out, hipStream_t stream);
 
 }  // namespace dpow

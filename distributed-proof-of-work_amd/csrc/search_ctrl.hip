@@ -88,7 +88,16 @@ __global__ void context_init_kernel(Ctrl *ctrl, uint32_t n_ctrl, unsigned long l
     }
     for (uint32_t i = threadIdx.x; i < n_claims; i += blockDim.x) claims[i] = 0ull;
 }
+__global__ void clock_probe_kernel(unsigned long long *out) {
+    if (threadIdx.x == 0)
+        __hip_atomic_store(out, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 }  // namespace
+
+hipError_t clock_probe(unsigned long long *out, hipStream_t stream) {
+    hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, stream, out);
+    return hipGetLastError();
+}
 
 hipError_t context_init(Ctrl *ctrl, uint32_t n_ctrl, unsigned long long *claims, uint32_t n_claims,
                         hipStream_t stream) {

@@ -48,6 +48,14 @@ DPOW_MAX_NONCE = 1024
 EPROTO, ETIMEOUT = -6, -7
 
 
+class LaunchTime(ctypes.Structure):
+    """dpow_diag_launch_time (include/dpow_diag.h)."""
+    _fields_ = [("seq", ctypes.c_uint64), ("kind", ctypes.c_int32), ("recorded", ctypes.c_int32),
+                ("queued_ns", ctypes.c_int64), ("seen_ns", ctypes.c_int64),
+                ("t_start_tick", ctypes.c_uint64), ("t_end_tick", ctypes.c_uint64),
+                ("candidates", ctypes.c_uint64), ("g_end", ctypes.c_uint64), ("best", ctypes.c_uint64)]
+
+
 class WorkerResult(ctypes.Structure):
     _fields_ = [("num_trailing_zeros", ctypes.c_uint32), ("worker_byte", ctypes.c_uint32),
                 ("has_secret", ctypes.c_uint32), ("secret_len", ctypes.c_uint32), ("error", ctypes.c_int32),
@@ -223,6 +231,9 @@ def lib():
         "dpow_diag_blocks_per_cu": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
         "dpow_diag_search_times": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "dpow_diag_node_post_at": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_int64]),
+        "dpow_diag_search_launches": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(LaunchTime),
+                                                     ctypes.c_size_t]),
+        "dpow_diag_clock_sync": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
         "dpow_worker_new": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
         "dpow_worker_free": (None, [vp]),
         "dpow_worker_mine": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,

@@ -123,6 +123,7 @@ class NodeBoard:
         self._votes = self._base + self.SLOTS * self.SLOT_BYTES
         self._epoch = 0
         self._calls = 0
+        self._native = None  # node_mine's dpow_node_mine call state (_NativeCall), built at first use
 
     @property
     def shared(self) -> bool:
@@ -291,36 +292,66 @@ def first_window_k(num_trailing_zeros: int, world: int, factor: float) -> int:
 NODE_FIRST_FACTOR = float(__import__("os").environ.get("DPOW_NODE_FIRST", "0") or 0)
 
 
+def _miner_class():
+    from .search import Miner
+    return Miner
+
+
+class _NativeCall:
+    """The ctypes state of one board's dpow_node_mine calls, built once: the bound entry
+    point, the out-parameters and their pointers, the slot-reset entry point.  A node search
+    of tens of microseconds paid ~5 us of Python (imports, ctypes objects, lookups) around the
+    call, each time (tools/search_timeline.py)."""
+
+    def __init__(self):
+        import ctypes
+
+        from ._lib import DPOW_MAX_SECRET, lib
+        L = lib()
+        self.fn = L.dpow_node_mine
+        self.reset = L.dpow_node_slot_reset
+        self.last_error = L.dpow_last_error
+        self.epoch = ctypes.c_uint64(0)
+        self.best = ctypes.c_uint64(DPOW_NO_HIT)
+        self.sec = (ctypes.c_uint8 * DPOW_MAX_SECRET)()
+        self.slen = ctypes.c_size_t()
+        self.batches = ctypes.c_uint32()
+        self.p_epoch = ctypes.pointer(self.epoch)
+        self.p_best = ctypes.pointer(self.best)
+        self.p_slen = ctypes.pointer(self.slen)
+        self.p_batches = ctypes.pointer(self.batches)
+
+
 def _node_mine_native(miner, board: "NodeBoard", nonce: Sequence[int], num_trailing_zeros: int, rank: int,
                       world: int, k_start: int, k_limit: int, batch_k: int, first_k: int) -> NodeResult:
     """node_mine over a board in one call of dpow_node_mine (include/dpow.h, ABI 4): the batch
     loop, the Found fan-out and the node vote in C, no Python round per batch."""
-    import ctypes
-
-    from ._lib import DPOW_MAX_SECRET, DpowError, lib
-    L = lib()
-    slot = board.begin()
+    nc = board._native
+    if nc is None:
+        nc = board._native = _NativeCall()
+    calls = board._calls
+    slot = board._base + (calls % board.SLOTS) * board.SLOT_BYTES
     n = bytes(nonce)
-    epoch = ctypes.c_uint64(board._epoch)
-    best = ctypes.c_uint64(DPOW_NO_HIT)
-    sec = (ctypes.c_uint8 * DPOW_MAX_SECRET)()
-    slen = ctypes.c_size_t()
-    batches = ctypes.c_uint32()
+    nc.epoch.value = board._epoch
     votes = board._votes if (board.shared and board.world == world) else None
     try:
-        rc = L.dpow_node_mine(miner._ctx, slot, votes, rank, world, ctypes.byref(epoch), board.VOTE_TIMEOUT_NS,
-                              n, len(n), num_trailing_zeros, k_start, k_limit, first_k, batch_k,
-                              ctypes.byref(best), sec, ctypes.byref(slen), ctypes.byref(batches))
+        rc = nc.fn(miner._ctx, slot, votes, rank, world, nc.p_epoch, board.VOTE_TIMEOUT_NS, n, len(n),
+                   num_trailing_zeros, k_start, k_limit, first_k, batch_k, nc.p_best, nc.sec, nc.p_slen,
+                   nc.p_batches)
     finally:
-        board._epoch = epoch.value
-        board.end()
-    if rc == EPROTO:
-        raise NodeError(f"rank {rank}: {L.dpow_last_error().decode()}")
-    if rc < 0:
-        raise DpowError(rc, f"rank {rank}: dpow_node_mine: {L.dpow_last_error().decode()}")
+        board._epoch = nc.epoch.value
+        # board.end(): the slot two calls ahead is reset for its next user
+        nc.reset(board._base + ((calls + 2) % board.SLOTS) * board.SLOT_BYTES)
+        board._calls = calls + 1
     if rc == FOUND:
-        return NodeResult(FOUND, best.value, bytes(sec[:slen.value]), owner_rank(best.value, world), batches.value)
-    return NodeResult(rc, batches=batches.value)
+        best = nc.best.value
+        return NodeResult(FOUND, best, bytes(nc.sec[:nc.slen.value]), owner_rank(best, world), nc.batches.value)
+    if rc == EPROTO:
+        raise NodeError(f"rank {rank}: {nc.last_error().decode()}")
+    if rc < 0:
+        from ._lib import DpowError
+        raise DpowError(rc, f"rank {rank}: dpow_node_mine: {nc.last_error().decode()}")
+    return NodeResult(rc, batches=nc.batches.value)
 
 
 def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int, rank: int, world: int,
@@ -362,15 +393,17 @@ def node_mine(search_fn: Callable, nonce: Sequence[int], num_trailing_zeros: int
     (dpow_node_mine, round 5) -- the same windows, votes and answers, without a Python round
     per batch (4-5 us per node search).  search_fn and attach_fn are then unused.
     """
+    if miner is not None and board is not None and batch_k is None and isinstance(miner, _miner_class()):
+        wbits = world.bit_length() - 1
+        if world < 1 or world & (world - 1):
+            partition_of_rank(rank, world)  # raises
+        bk = max(1, BOARD_BATCH_CANDIDATES >> (8 - wbits % 9))
+        return _node_mine_native(miner, board, nonce, num_trailing_zeros, rank, world, k_start, k_limit, bk,
+                                 first_window_k(num_trailing_zeros, world, NODE_FIRST_FACTOR))
     import torch
     import torch.distributed as dist
 
     wb, wbits = partition_of_rank(rank, world)
-    from .search import Miner
-    if isinstance(miner, Miner) and board is not None and batch_k is None:
-        bk = max(1, BOARD_BATCH_CANDIDATES >> (8 - wbits % 9))
-        return _node_mine_native(miner, board, nonce, num_trailing_zeros, rank, world, k_start, k_limit, bk,
-                                 first_window_k(num_trailing_zeros, world, NODE_FIRST_FACTOR))
     if batch_k is None:
         cand = (BOARD_BATCH_CANDIDATES if board is not None and attach_fn is not None
                 else auto_batch_candidates(num_trailing_zeros, world))

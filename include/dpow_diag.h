@@ -98,6 +98,33 @@ uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t wor
  * DPOW_DIAG_SHARE_MAX (grid share cap).  Returns 0, or < 0 on error. */
 int dpow_diag_search_times(struct dpow_ctx *ctx, int64_t out[8]);
 
+/* The launches of the context's last dpow_search call, in launch order (round 5): the
+ * host's CLOCK_MONOTONIC ns when each was queued and when its completion record was
+ * consumed (-1: not consumed, e.g. left in flight behind a hit or a covered bound), and
+ * the record's device s_memrealtime stamps (100 MHz; the k = 0 kernel's own, an md5
+ * launch's start as its watcher stamps it and its end as the last workgroup publishes it;
+ * 0 while the record is not written).  *t0_ns: the search's start (CLOCK_MONOTONIC ns).
+ * Returns the number of launches (at most 32 are kept; only max_launches are written),
+ * or < 0 on error.  dpow_diag_clock_sync maps the device stamps to host time. */
+typedef struct dpow_diag_launch_time {
+    uint64_t seq;                 /* launch sequence number of the context */
+    int32_t kind;                 /* 0 the k = 0 kernel, 1 an md5 launch */
+    int32_t recorded;             /* its completion record is written */
+    int64_t queued_ns, seen_ns;   /* host: queued, record consumed (-1: not) */
+    uint64_t t_start_tick, t_end_tick;  /* device s_memrealtime stamps of the record */
+    uint64_t candidates, g_end;   /* local indices; global indices below g_end */
+    uint64_t best;                /* the record's best (DPOW_NO_HIT: none) */
+} dpow_diag_launch_time;
+int dpow_diag_search_launches(struct dpow_ctx *ctx, int64_t *t0_ns, dpow_diag_launch_time *out,
+                              size_t max_launches);
+
+/* Pairs the device's s_memrealtime clock with the host's CLOCK_MONOTONIC: `reps` one-thread
+ * kernels on the context's stream stamp s_memrealtime into pinned host memory while the
+ * host spins on it.  *offset_ns = min over reps of (host ns when the stamp was seen -
+ * stamp x 10 ns), so host ns ~= tick x 10 + *offset_ns, late by the stamp's write latency
+ * to host memory (~1 us).  Waits for the stream first.  Returns 0, or < 0 on error. */
+int dpow_diag_clock_sync(struct dpow_ctx *ctx, int reps, int64_t *offset_ns);
+
 /* Node emulation on one GPU (tools/node_probe.py): post global_idx to a node slot
  * (dpow_node_post) from a detached native thread at CLOCK_MONOTONIC time t_ns, as another
  * rank's process would -- off the caller's thread and its Python interpreter lock.

@@ -128,6 +128,9 @@ def test_null_arguments_are_errors_not_crashes():
     sec, sl = (ctypes.c_uint8 * 16)(), ctypes.c_size_t()
     assert L.dpow_node_mine(None, None, None, 0, 2, ctypes.byref(e), 0, b"\x01", 1, 3, 0, 1, 0, 1,
                             ctypes.byref(b), sec, ctypes.byref(sl), ctypes.byref(n)) == -1
+    t0 = ctypes.c_int64(0)
+    assert L.dpow_diag_search_launches(None, ctypes.byref(t0), None, 0) == -1
+    assert L.dpow_diag_clock_sync(None, 4, ctypes.byref(t0)) == -1
     L.dpow_close(None)  # no-op
 
 

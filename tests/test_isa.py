@@ -85,3 +85,17 @@ def test_claim_ahead_latency_hidden(kernel_110):
                 hidden |= a2 - base > hash_lo
                 break
     assert hidden, "every claim atomic is waited for before the hash block"
+
+
+def test_sweep_kernel_hash_block_placement():
+    """The sweep's kernel (<1,1,0> with the D-equality test) keeps its hash block at round 4's
+    offset modulo 256 (0x68): every watcher change re-runs the kernel's register allocation and
+    moves its code, and a 4-16 byte move of the hash block alone cost the sweep 0.3-0.5 % in
+    round 5 (md5_search_kernel.h DPOW_PAD_4B restores the offset)."""
+    import isa_loop
+    text = isa_loop.disasm(os.path.join(ROOT, "distributed-proof-of-work_amd", "csrc"), 1, 0, [])
+    lines = isa_loop.kernel_lines(text, 1, 1, 0, 1)
+    lo, hi, c = max(isa_loop.hash_block_mix(lines), key=lambda b: sum(b[2].values()))
+    assert lo % 256 == 0x68, hex(lo)
+    assert sum(v for k, v in c.items() if k.startswith("v_")) == 494
+

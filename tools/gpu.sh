@@ -13,8 +13,10 @@
 #                    `bench.py --gpus 8` (gloo, --same-device), the rocprofv3 kernel-trace and
 #                    PMC passes of the bench (tools/profile_gpu.sh)
 #   node [runs] [G,..] [small]   the emulated node alone
-#   node-small-ab name=lib.so ...   the emulated node's small cases per library (A/B of builds)
+#   node-small-ab name=lib.so ...   the emulated node's small cases per library (A/B of builds;
+#                    NODE_RUNS runs per case, default 3)
 #   timeline [G,..]  host timelines of one GPU's and the node ranks' searches (tools/owner_timeline.py)
+#   stl [G,..] [cases]   host + device timeline of small searches on one clock (tools/search_timeline.py)
 #   trace [G,..] [cases]   per-wave traces (diag build distpow/libdpow_trace.so, tools/wave_trace_node.py)
 #   layouts [log2 rounds lengths]   GPU tests, the layout check, the layout sweep (tools/layout_sweep.py)
 #   rehearse [N]     N gloo ranks of bench.py on device 0 (the driver's N > 1 path, one GPU)
@@ -72,10 +74,14 @@ node-small-ab)  # the emulated 2/4/8-GPU node's small cases per library, twice, 
     for rnd in 1 2; do
         for spec in "$@"; do
             name=${spec%%=*}; lib=${spec#*=}
-            DPOW_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/node_probe.py 3 2,4,8 small \
+            DPOW_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/node_probe.py ${NODE_RUNS:-3} 2,4,8 small \
                 > $out/node_${name}_$rnd.json 2> $out/node_${name}_$rnd.err || exit $?
         done
     done ;;
+stl)  # the timeline with the product library, then with the diag build's per-wave records
+    timeout -k 10 300 python3 -u tools/search_timeline.py "$@" > $out/search_timeline.json 2> $out/search_timeline.err &&
+    DPOW_LIB_PATH=distributed-proof-of-work_amd/distpow/libdpow_trace.so timeout -k 10 300 \
+        python3 -u tools/search_timeline.py "$@" > $out/search_timeline_trace.json 2> $out/search_timeline_trace.err ;;
 timeline) timeout -k 10 300 python3 -u tools/owner_timeline.py "${1:-2,4,8}" > $out/owner_timeline.json 2> $out/owner_timeline.err ;;
 trace)
     DPOW_LIB_PATH=distributed-proof-of-work_amd/distpow/libdpow_trace.so timeout -k 10 300 \

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/prctl.h>
 #include <time.h>
 
@@ -933,17 +935,35 @@ int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, u
     __atomic_store_n(&mine.epoch, epoch, __ATOMIC_RELEASE);
     int64_t acc[3] = {in[0], in[1], in[2]};
     const int64_t t0 = now_ns();
+    // Spin while the other ranks are expected soon (a node's ranks end a search within tens of
+    // microseconds of each other), then poll every 2 us with the thread's timer slack lowered
+    // (a 2 us nanosleep under Linux's default 50 us slack wakes ~50 us late).
+    constexpr int64_t kVoteSpinNs = 500000;
+    long old_slack = -1;
+    struct SlackRestore {
+        long &old;
+        ~SlackRestore() {
+            if (old >= 0) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)old, 0UL, 0UL, 0UL);
+        }
+    } slack_restore{old_slack};
     for (uint32_t r = 0; r < world; ++r) {
         if (r == rank) continue;
         const dpow_node_vote_entry &e = votes[2 * r + (epoch & 1)];
         for (uint64_t it = 0; __atomic_load_n(&e.epoch, __ATOMIC_ACQUIRE) != epoch; ++it) {
-            if (it < 4096) {
+            if (it % 64 != 0 || now_ns() - t0 < std::min(kVoteSpinNs, timeout_ns)) {
                 __builtin_ia32_pause();
                 continue;
             }
             if (now_ns() - t0 > timeout_ns)
                 return set_error(DPOW_EPROTO, "dpow_node_vote: rank " + std::to_string(r) + " did not vote at epoch " +
                                                   std::to_string(epoch));
+            if (old_slack < 0) {
+                const int sl = prctl(PR_GET_TIMERSLACK, 0UL, 0UL, 0UL, 0UL);
+                if (sl > 0) {
+                    old_slack = sl;
+                    (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+                }
+            }
             const struct timespec d = {0, 2000};
             nanosleep(&d, nullptr);
         }
@@ -1102,6 +1122,85 @@ int dpow_diag_node_post_at(dpow_node_slot *slot, uint64_t global_idx, int64_t t_
             }
         }).detach();
     }
+    return 0;
+}
+
+int dpow_diag_vote_latency(uint32_t world, int reps, double *last_us, double *all_us) {
+    if (world < 2 || world > 256 || reps < 1 || !last_us || !all_us)
+        return set_error(DPOW_EINVAL, "dpow_diag_vote_latency: world in [2, 256], reps >= 1, outputs non-NULL");
+    void *mem = aligned_alloc(64, (size_t)2 * world * sizeof(dpow_node_vote_entry));
+    if (!mem) return set_error(DPOW_EINVAL, "dpow_diag_vote_latency: out of memory");
+    memset(mem, 0, (size_t)2 * world * sizeof(dpow_node_vote_entry));
+    auto *votes = static_cast<dpow_node_vote_entry *>(mem);
+    // The ranks on CPUs spread over this thread's affinity set, as a node's processes would be.
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    std::vector<int> cpus;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) == 0)
+        for (int i = 0; i < CPU_SETSIZE; ++i)
+            if (CPU_ISSET(i, &allowed)) cpus.push_back(i);
+    auto pin = [&](uint32_t r) {
+        if (cpus.empty()) return;
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(cpus[(size_t)r * cpus.size() / world], &one);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+    };
+    std::atomic<int> go{0};
+    std::vector<std::atomic<int64_t>> done_at(world);
+    for (auto &d : done_at) d.store(0);
+    std::atomic<int> failed{0};
+    std::vector<std::thread> others;
+    for (uint32_t r = 1; r < world; ++r)
+        others.emplace_back([&, r]() {
+            pin(r);
+            for (int rep = 1; rep <= reps; ++rep) {
+                while (go.load(std::memory_order_acquire) < rep) __builtin_ia32_pause();
+                const int64_t in[3] = {(int64_t)(1000 + r), 1, 1};
+                int64_t out[3];
+                if (dpow_node_vote(votes, r, world, (uint64_t)rep, in, out, 1000000000) != 0) failed.store(1);
+                done_at[r].store(now_ns(), std::memory_order_release);
+                while (go.load(std::memory_order_acquire) == rep) __builtin_ia32_pause();  // rank 0 collects
+            }
+        });
+    // Rank 0 (this thread) arrives last: it waits until every other rank has voted and sits in
+    // the vote's spin, then votes; last_us is its own vote, all_us the time until every rank
+    // holds the result -- the node vote's share of a node's time-to-secret.
+    cpu_set_t caller;
+    const bool have_caller = pthread_getaffinity_np(pthread_self(), sizeof caller, &caller) == 0;
+    pin(0);
+    std::vector<double> last, all;
+    int64_t t_prev_done = 0;
+    for (int rep = 1; rep <= reps && !failed.load(); ++rep) {
+        go.store(rep, std::memory_order_release);
+        for (uint32_t r = 1; r < world; ++r)
+            while (__atomic_load_n(&votes[2 * r + (rep & 1)].epoch, __ATOMIC_ACQUIRE) != (uint64_t)rep)
+                __builtin_ia32_pause();
+        for (const int64_t t_wait = now_ns(); now_ns() - t_wait < 2000;) __builtin_ia32_pause();
+        const int64_t t0 = now_ns();
+        const int64_t in[3] = {1000, 1, 1};
+        int64_t out[3];
+        if (dpow_node_vote(votes, 0, world, (uint64_t)rep, in, out, 1000000000) != 0 || out[0] != 1000) failed.store(1);
+        const int64_t t1 = now_ns();
+        int64_t t_all = t1;
+        for (uint32_t r = 1; r < world; ++r) {
+            int64_t t;
+            while ((t = done_at[r].load(std::memory_order_acquire)) <= t_prev_done) __builtin_ia32_pause();
+            t_all = std::max(t_all, t);
+        }
+        t_prev_done = t_all;
+        last.push_back((t1 - t0) / 1e3);
+        all.push_back((t_all - t0) / 1e3);
+    }
+    go.store(reps + 1, std::memory_order_release);
+    for (auto &t : others) t.join();
+    if (have_caller) (void)pthread_setaffinity_np(pthread_self(), sizeof caller, &caller);
+    free(mem);
+    if (failed.load() || last.empty()) return set_error(DPOW_EPROTO, "dpow_diag_vote_latency: a vote failed");
+    std::sort(last.begin(), last.end());
+    std::sort(all.begin(), all.end());
+    *last_us = last[last.size() / 2];
+    *all_us = all[all.size() / 2];
     return 0;
 }
 

@@ -234,6 +234,8 @@ def lib():
         "dpow_diag_search_launches": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(LaunchTime),
                                                      ctypes.c_size_t]),
         "dpow_diag_clock_sync": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+        "dpow_diag_vote_latency": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                  ctypes.POINTER(ctypes.c_double)]),
         "dpow_worker_new": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
         "dpow_worker_free": (None, [vp]),
         "dpow_worker_mine": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,

@@ -125,6 +125,13 @@ int dpow_diag_search_launches(struct dpow_ctx *ctx, int64_t *t0_ns, dpow_diag_la
  * to host memory (~1 us).  Waits for the stream first.  Returns 0, or < 0 on error. */
 int dpow_diag_clock_sync(struct dpow_ctx *ctx, int reps, int64_t *offset_ns);
 
+/* The node vote's cost to a node's time-to-secret (dpow_node_vote, round 5), on this host:
+ * `world` threads on CPUs spread over the caller's affinity set; ranks 1..world-1 vote first
+ * and wait in the vote, rank 0 (the calling thread) votes last.  *last_us: rank 0's vote call;
+ * *all_us: from rank 0's call until every rank holds the result.  Medians over `reps`.
+ * tools/node_probe.py adds *all_us to the slowest rank's time.  Returns 0, or < 0 on error. */
+int dpow_diag_vote_latency(uint32_t world, int reps, double *last_us, double *all_us);
+
 /* Node emulation on one GPU (tools/node_probe.py): post global_idx to a node slot
  * (dpow_node_post) from a detached native thread at CLOCK_MONOTONIC time t_ns, as another
  * rank's process would -- off the caller's thread and its Python interpreter lock.

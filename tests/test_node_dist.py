@@ -404,6 +404,24 @@ def test_node_vote_shared_memory():
         shm.unlink()
 
 
+def test_vote_latency_diagnostic():
+    """dpow_diag_vote_latency (tools/node_probe.py's node-vote cost): the vote's MIN holds with
+    the last rank arriving after the others wait, the medians are finite, the caller's CPU
+    affinity is left as it was; bad arguments are errors."""
+    import ctypes
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-proof-of-work_amd"))
+    from distpow._lib import lib
+    before = os.sched_getaffinity(0)
+    last, all_ = ctypes.c_double(), ctypes.c_double()
+    assert lib().dpow_diag_vote_latency(2, 50, ctypes.byref(last), ctypes.byref(all_)) == 0
+    assert 0 <= last.value <= all_.value < 1e6
+    assert os.sched_getaffinity(0) == before
+    assert lib().dpow_diag_vote_latency(1, 50, ctypes.byref(last), ctypes.byref(all_)) == -1
+    assert lib().dpow_diag_vote_latency(2, 0, ctypes.byref(last), ctypes.byref(all_)) == -1
+
+
 def _worker_board_fail(rank, world, port, out_q):
     """rank 0 cannot create the shared-memory segment (e.g. /dev/shm full):
     every rank returns None from NodeBoard.create together, at once, instead of the

@@ -18,10 +18,13 @@ hit, or a non-owner's time to notice the posted hit and drain.  This runs
 
 and reports max over ranks, next to one GPU's Miner.mine (G1).  node_mine runs here
 without a process group or a shared board, so its batch boundary is a no-op on the host
-(no tensors, no collective): the real node adds one node vote per batch on a shared board (NodeBoard,
-2.5 us median in the 2-rank rehearsal, profiles/r03_bench_n2_rehearsal.json), or one RCCL
-all-reduce (33 us at world 1) across hosts.  The ranks run one after another, each with
-the whole GPU; the 8-GPU number itself is the driver's (bench.py --gpus 8).
+(no tensors, no collective): the real node adds one node vote per batch on a shared board
+(NodeBoard), measured on this host by dpow_diag_vote_latency -- G threads on CPUs spread over
+the process's affinity set, the last rank voting after the others wait in the vote: the time
+until every rank holds the result (round 4 added a constant 3.5 us, the 2-rank rehearsal's
+median of a Python-level vote after a gloo barrier).  Across hosts it is one RCCL all-reduce
+(33 us at world 1).  The ranks run one after another, each with the whole GPU; the 8-GPU
+number itself is the driver's (bench.py --gpus 8).
 """
 import ctypes
 import json
@@ -38,10 +41,8 @@ import distpow  # noqa: E402
 from distpow.node import NodeBoard, node_mine, owner_rank  # noqa: E402
 
 
-# The real node's batch boundary on a shared board: one node vote (NodeBoard.vote), 2.5-3.5 us
-# median in the 2- and 8-rank rehearsals (profiles/r03_bench_n2_rehearsal.json): added to the
-# slowest rank's time.  (Here node_mine runs without a process group or a shared board.)
-NODE_VOTE_MS = 0.0035
+# DPOW_NODE_VOTE_US: a fixed node-vote cost instead of the measured one (round 4: 3.5)
+VOTE_US_FIXED = os.environ.get("DPOW_NODE_VOTE_US")
 # The rank's search through the native loop (dpow_node_mine, as bench.py runs it) unless
 # DPOW_NODE_PY=1 (round 4's Python loop over Miner.search).
 NATIVE = os.environ.get("DPOW_NODE_PY") != "1"
@@ -63,6 +64,17 @@ def main():
     out = {"note": __doc__.strip().splitlines()[0], "g1_ms": {}, "node_ms": {}}
     board = NodeBoard.local()
     lib = distpow.lib()
+    # the node vote's cost per G on this host (the slowest rank's time + it = the node's)
+    vote_ms = {}
+    for G in gs:
+        if VOTE_US_FIXED:
+            vote_ms[G] = float(VOTE_US_FIXED) / 1e3
+            continue
+        last, all_ = ctypes.c_double(), ctypes.c_double()
+        assert lib.dpow_diag_vote_latency(G, 400, ctypes.byref(last), ctypes.byref(all_)) == 0, \
+            lib.dpow_last_error().decode()
+        vote_ms[G] = all_.value / 1e3
+    out["vote_us"] = {str(G): round(v * 1e3, 3) for G, v in vote_ms.items()}
     with distpow.Miner(0) as m:
         search = lambda *a: m.search(*a[:6], bound=a[6])  # noqa: E731
         m.search([1, 2, 3, 4], 32, 0, 0, 1 << 24, (1 << 24) + (1 << 26))  # warm
@@ -150,7 +162,7 @@ def main():
                     per_rank.append(med(ts))
                 key = f"G{G} {bytes(nonce).hex()}/{n}"
                 g1 = out["g1_ms"][f"{bytes(nonce).hex()}/{n}"]
-                node = max(per_rank) + NODE_VOTE_MS  # the slowest rank plus the node's one vote
+                node = max(per_rank) + vote_ms[G]  # the slowest rank plus the node's one vote
                 out["node_ms"][key] = {"global_idx": g, "owner": o, "owner_ms": per_rank[o],
                                        "max_rank_ms": max(per_rank), "per_rank_ms": per_rank,
                                        "node_ms": round(node, 3), "speedup_vs_g1": round(g1 / node, 2)}

@@ -81,14 +81,28 @@ constexpr uint32_t kClaimSlot = kClaimCounters * kClaimStride;  // one launch's 
 // previous search's launches (Launch::ctrl_next), or at dpow_open -- so a search needs
 // no reset kernel in front of its first launch.
 constexpr unsigned long long kNoHit = 0x7FFFFFFFFFFFFFFFull;  // = DPOW_NO_HIT (include/dpow.h)
+#ifndef DPOW_CTRL_SPLIT
+#define DPOW_CTRL_SPLIT 1  // Ctrl::done on a 128-byte line of its own (A/B switch)
+#endif
 struct Ctrl {
     unsigned long long best;  // min global index found (kNoHit = none), atomicMin target
     uint32_t stop;            // set by the watcher when the host cancel flag is raised
+#if DPOW_CTRL_SPLIT
+    // Every wave loads best and stop once per poll group: the retirement count's atomics
+    // (one per workgroup, at the end of a launch) queue behind those loads on a shared line.
+    uint32_t pad0_;
+    unsigned long long pad1_[14];
+#endif
     uint32_t done;            // worker workgroups retired (cumulative within one search)
+#if DPOW_CTRL_SPLIT
+    uint32_t pad2_[31];
+#endif
 };
+constexpr uint32_t kCtrlLine = DPOW_CTRL_SPLIT ? 256 : 128;  // bytes per ring entry
 constexpr uint32_t kCtrlRing = 4;
-constexpr uint32_t kCtrlStride = 128 / sizeof(Ctrl);  // Ctrl units between ring entries
-static_assert((kCtrlRing & (kCtrlRing - 1)) == 0 && 128 % sizeof(Ctrl) == 0, "the ring is aligned to its size");
+constexpr uint32_t kCtrlStride = kCtrlLine / sizeof(Ctrl);  // Ctrl units between ring entries
+static_assert((kCtrlRing & (kCtrlRing - 1)) == 0 && kCtrlLine % sizeof(Ctrl) == 0, "the ring is aligned to its size");
+static_assert(!DPOW_CTRL_SPLIT || (sizeof(Ctrl) == 256 && __builtin_offsetof(Ctrl, done) == 128), "done on its own line");
 
 // Host-visible completion record of one launch (pinned, host-coherent, mapped).
 // The launch's last retiring workgroup writes it: the

@@ -12,6 +12,7 @@
 // against Ctrl::best / Ctrl::stop before hashing), in stream order ahead of
 // the next search on the context.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
@@ -1137,8 +1138,20 @@ int dpow_diag_vote_latency(uint32_t world, int reps, double *last_us, double *al
     CPU_ZERO(&allowed);
     std::vector<int> cpus;
     if (sched_getaffinity(0, sizeof allowed, &allowed) == 0)
-        for (int i = 0; i < CPU_SETSIZE; ++i)
-            if (CPU_ISSET(i, &allowed)) cpus.push_back(i);
+        for (int i = 0; i < CPU_SETSIZE; ++i) {
+            if (!CPU_ISSET(i, &allowed)) continue;
+            // one hardware thread per core (the first of its siblings): two ranks on SMT
+            // siblings would share a core's caches, which a node's processes do not
+            char path[96];
+            snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", i);
+            if (FILE *f = fopen(path, "r")) {
+                int first = -1;
+                const int n = fscanf(f, "%d", &first);
+                fclose(f);
+                if (n == 1 && first != i) continue;
+            }
+            cpus.push_back(i);
+        }
     auto pin = [&](uint32_t r) {
         if (cpus.empty()) return;
         cpu_set_t one;

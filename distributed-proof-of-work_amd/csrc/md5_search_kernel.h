@@ -65,6 +65,12 @@ namespace DPOW_KNS {
 #ifndef DPOW_WATCH_BATCH
 #define DPOW_WATCH_BATCH 1  // the watcher loads a poll's words together (0: round 4's poll; A/B switch)
 #endif
+#ifndef DPOW_XCD_RETIRE
+// Retirement counted per claim counter, then on Ctrl::done (A/B switch; 2: out of line): in the
+// chunk-length-spanning units only -- the launches of short searches, below k = 2^24 -- so
+// that the other units' kernels (the sweep's among them) keep their code.
+#define DPOW_XCD_RETIRE (DPOW_VLS ? 1 : 0)
+#endif
 #ifndef DPOW_HIT_EARLY
 #define DPOW_HIT_EARLY 0  // 1: a wave's hit goes to the early-hit word from the hit path (A/B switch)
 #endif
@@ -760,6 +766,30 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 #endif
 }
 
+#if DPOW_XCD_RETIRE == 2
+// The retirement of one worker workgroup (its thread 0), out of line so that its code does not
+// enter the hash kernels' register allocation: counted per claim counter first (worker block b
+// serves counter (b - 1) % 8, its XCD's) on a word of that counter's line, and the counter's
+// last workgroup adds the counter's count to Ctrl::done -- a launch's few hundred to ~1500
+// retirements no longer queue on one line (~100 atomics per us) at its end.  The workgroup
+// that completes Ctrl::done publishes the record.
+__device__ __attribute__((noinline)) void retire(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim,
+                                                 Ctrl *ctrl_next, uint32_t done_target) {
+    const uint32_t n_wg = gridDim.x - 1u;
+    const uint32_t xr = (blockIdx.x - 1u) % kClaimCounters;
+    const uint32_t nx = n_wg / kClaimCounters + (xr < n_wg % kClaimCounters ? 1u : 0u);
+    unsigned long long *const xc = claim + xr * kClaimStride + 2;
+    const unsigned long long px = __hip_atomic_fetch_add(xc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (px + 1ull != (unsigned long long)nx) return;
+    __hip_atomic_store(xc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the slot's next launch
+    const uint32_t prev = __hip_atomic_fetch_add(&ctrl->done, nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if DPOW_WAVE_TRACE
+    if (prev + nx == done_target) g_wave_trace[kTraceFields * (kTraceWaves - 2) + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (prev + nx == done_target) publish(ctrl, snap, seq, claim, ctrl_next);
+}
+#endif
+
 // Workgroup 0, one lane: relays the host cancel flag to Ctrl::stop while the
 // launch runs; exits once every worker workgroup has retired.  A launch that
 // was still queued when its search returned CANCELLED stops too, even after
@@ -1387,6 +1417,41 @@ DPOW_DEV void search_body(const Launch &L) {
 #if DPOW_WAVE_TRACE
         const unsigned long long t_bar = __builtin_amdgcn_s_memrealtime();
 #endif
+#if DPOW_XCD_RETIRE == 2
+#if DPOW_WAVE_TRACE
+        {
+            unsigned long long *r = g_wave_trace + kTraceFields * (kTraceWaves - 2);
+            r[0] = t_claims;  // (every workgroup writes; the publisher's retire() writes r[2] last)
+            r[1] = t_bar;
+        }
+#endif
+        retire(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr, L.done_target);
+#elif DPOW_XCD_RETIRE
+        // Retirement is counted per claim counter first (worker block b serves counter
+        // (b - 1) % 8, its XCD's) on a word of that counter's line, and the counter's last
+        // workgroup adds the counter's count to Ctrl::done: a launch's few hundred to ~1500
+        // retirements no longer queue on one line (~100 atomics per us) at its end.
+        const uint32_t n_wg = gridDim.x - 1u;
+        const uint32_t xr = (blockIdx.x - 1u) % kClaimCounters;
+        const uint32_t nx = n_wg / kClaimCounters + (xr < n_wg % kClaimCounters ? 1u : 0u);
+        unsigned long long *const xc = L.claim + xr * kClaimStride + 2;
+        const unsigned long long px = __hip_atomic_fetch_add(xc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (px + 1ull == (unsigned long long)nx) {
+            // every retirement of this counter is in: zero it for the slot's next launch
+            __hip_atomic_store(xc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if DPOW_WAVE_TRACE
+            if (prev + nx == L.done_target) {  // the publisher's retirement: slot kTraceWaves - 2
+                unsigned long long *r = g_wave_trace + kTraceFields * (kTraceWaves - 2);
+                r[0] = t_claims;
+                r[1] = t_bar;
+                r[2] = __builtin_amdgcn_s_memrealtime() + (prev & 0);
+            }
+#endif
+            if (prev + nx == L.done_target)
+                publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
+        }
+#else
         const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if DPOW_WAVE_TRACE
         if (prev + 1u == L.done_target) {  // the publisher's retirement: slot kTraceWaves - 2
@@ -1397,6 +1462,7 @@ DPOW_DEV void search_body(const Launch &L) {
         }
 #endif
         if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
+#endif
     }
 }
 

@@ -803,3 +803,34 @@ def test_concurrent_searches_share_the_gpu(golden):
     finally:
         for m in miners:
             m.close()
+
+
+def test_windows_from_k0_vs_oracle(miner, oracle):
+    """Windows from k = 0 (the search's k = 0 kernel, search_ctrl.hip, ahead of its first md5
+    launch; k = 0 alone, k = 0 with one more k, with chunk lengths 1-2, 1-3): hits at k = 0 and
+    above it, partition widths 0-5 bits, nonces of 4, 5, 8 and 12 bytes, a bound inside k = 0."""
+    rnd = random.Random(5150)
+    checked = 0
+    for nlen in (4, 5, 8, 12):
+        for ntz in (1, 2, 3):
+            for wbits in (0, 1, 3, 5):
+                nonce = [rnd.randrange(256) for _ in range(nlen)]
+                wb = rnd.randrange(1 << wbits)
+                for k1 in (1, 2, 300, 70000):
+                    exp = oracle.mine_window(nonce, ntz, wb, wbits, 0, k1)
+                    r = miner.search(nonce, ntz, wb, wbits, 0, k1)
+                    if exp is None:
+                        assert r.status == EXHAUSTED, (nonce, ntz, wb, wbits, k1, r)
+                    else:
+                        assert r.status == FOUND and (list(r.secret), r.global_idx) == (exp[0], exp[1]), \
+                            (nonce, ntz, wb, wbits, k1, r, exp)
+                    checked += 1
+                # a bound inside k = 0: only a hit below it counts
+                exp = oracle.mine_window(nonce, ntz, wb, wbits, 0, 300)
+                if exp is not None and exp[1] < 256:
+                    r = miner.search(nonce, ntz, wb, wbits, 0, 300, bound=exp[1] + 1)
+                    assert r.status == FOUND and r.global_idx == exp[1], (nonce, ntz, wb, wbits, r, exp)
+                    r = miner.search(nonce, ntz, wb, wbits, 0, 300, bound=exp[1])
+                    assert r.status == EXHAUSTED, (nonce, ntz, wb, wbits, r, exp)
+    assert checked == 4 * 3 * 4 * 4
+

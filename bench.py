@@ -98,6 +98,25 @@ class _StreamTimer:
         return self.ev0.elapsed_time(self.ev1)
 
 
+# Where rank 0's JSON line goes: the process's original stdout when bench.py runs as a program
+# (guard_stdout), else sys.stdout (tests calling main() in-process).
+RESULT_OUT = None
+
+
+def guard_stdout():
+    """Keep stdout to the one JSON line: native libraries print to fd 1 themselves (RCCL's
+    version banner at communicator init, since round 5's world-1 RCCL group), so fd 1 becomes
+    a copy of stderr and the line goes to a duplicate of the original stdout."""
+    global RESULT_OUT
+    try:
+        sys.stdout.flush()
+        fd = os.dup(1)
+        os.dup2(2, 1)
+    except OSError:
+        return
+    RESULT_OUT = os.fdopen(fd, "w", buffering=1)
+
+
 class LineGuard:
     """Rank 0's one JSON line, printed exactly once: at the end, or with what was measured so
     far when the launcher stops this rank before the end (torch.distributed.run sends SIGTERM
@@ -140,8 +159,9 @@ class LineGuard:
                 return
             self.printed = True
             line = dict(self.line, **(extra or {}))
-            sys.stdout.write(json.dumps(line) + "\n")
-            sys.stdout.flush()
+            out = RESULT_OUT or sys.stdout
+            out.write(json.dumps(line) + "\n")
+            out.flush()
 
 
 def section(name, rank, fn, *a, **kw):
@@ -195,7 +215,8 @@ def main(argv=None, miner_factory=None, gpu=None):
         # process -- nothing here has touched the GPU yet -- and relay rank 0's line.
         sys.exit(launch_ranks(args))
     if args.print_launch:
-        print(json.dumps({"launch": None, "world_size": int(env_world or "1")}))
+        print(json.dumps({"launch": None, "world_size": int(env_world or "1")}), file=RESULT_OUT or sys.stdout,
+              flush=True)
         return
     world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
@@ -574,7 +595,7 @@ def launch_ranks(args):
     import subprocess
     cmd = launcher_argv(sys.argv[1:], args.gpus, free_port())
     if args.print_launch:
-        print(json.dumps({"launch": cmd, "world_size": args.gpus}))
+        print(json.dumps({"launch": cmd, "world_size": args.gpus}), file=RESULT_OUT or sys.stdout, flush=True)
         return 0
     if not args.same_device:
         ndev = torch.cuda.device_count()  # counts devices without initialising them
@@ -594,7 +615,7 @@ def launch_ranks(args):
             except ValueError:
                 pass
             if isinstance(rec, dict) and "metric" in rec:  # rank 0's result line
-                print(line.rstrip("\n"), flush=True)
+                print(line.rstrip("\n"), file=RESULT_OUT or sys.stdout, flush=True)
                 lines += 1
             else:
                 sys.stderr.write(line)
@@ -881,4 +902,5 @@ def cpu_baseline(threads, seconds):
 
 
 if __name__ == "__main__":
+    guard_stdout()
     main()

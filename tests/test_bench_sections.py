@@ -110,3 +110,18 @@ def test_sigterm_prints_the_sweep():
     assert p.returncode == 128 + signal.SIGTERM, (p.returncode, err[-3000:])
     rec = _line(out)
     assert rec["value"] > 0 and rec["ok"] is False and "signal" in rec["error"]
+
+
+def test_stdout_carries_only_the_json_line():
+    """bench.py as a program: a native library writing to fd 1 (RCCL prints its version banner
+    at communicator init) lands on stderr; rank 0's line is stdout's only line."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, %r); import bench; bench.guard_stdout(); "
+            "os.write(1, b'RCCL version : x\\n'); print('a python print'); g = bench.LineGuard(); "
+            "g.line = {'metric': 'm', 'value': 1}; g.emit()") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"metric": "m", "value": 1}'], r.stdout
+    assert "RCCL version" in r.stderr and "a python print" in r.stderr
+

@@ -678,15 +678,18 @@ struct PageEntry {
     void *page;
     bool foreign;                    // registered outside this library: never unregistered here
     std::vector<dpow_ctx *> holders;
+    char *dev = nullptr;             // the page's device alias (hipHostGetDevicePointer, once)
 };
 std::mutex g_page_mu;
 std::vector<PageEntry> g_pages;
 
 // A reference of ctx on `page` (registering it if no context holds it).  g_page_mu held.
-hipError_t page_hold_locked(dpow_ctx *c, void *page) {
+// *dev: the page's device alias.
+hipError_t page_hold_locked(dpow_ctx *c, void *page, char **dev) {
     for (PageEntry &pe : g_pages)
         if (pe.page == page) {
             if (std::find(pe.holders.begin(), pe.holders.end(), c) == pe.holders.end()) pe.holders.push_back(c);
+            *dev = pe.dev;
             return hipSuccess;
         }
     hipError_t e = hipHostRegister(page, 4096, hipHostRegisterMapped);
@@ -697,7 +700,13 @@ hipError_t page_hold_locked(dpow_ctx *c, void *page) {
         foreign = true;
     }
     if (e != hipSuccess) return e;
-    g_pages.push_back(PageEntry{page, foreign, {c}});
+    void *d = nullptr;
+    if ((e = hipHostGetDevicePointer(&d, page, 0)) != hipSuccess) {
+        if (!foreign) (void)hipHostUnregister(page);
+        return e;
+    }
+    g_pages.push_back(PageEntry{page, foreign, {c}, static_cast<char *>(d)});
+    *dev = static_cast<char *>(d);
     return hipSuccess;
 }
 
@@ -872,16 +881,24 @@ int dpow_node_attach(dpow_ctx *c, dpow_node_slot *slot) {
     // Map the slot's host page(s) for the watcher (fine-grained: hipHostRegister's default).
     const DeviceScope on_device(c->device);
     if (on_device.e != hipSuccess) return hip_fail(on_device.e, "hipSetDevice");
+    // The device alias of a slot within one page comes from its page's, looked up once when the
+    // page is registered: a node search attaches once per call, and hipHostGetDevicePointer per
+    // attach cost every node search its call (a board's slots are 64-byte aligned; a slot
+    // across two pages still asks the runtime).
     const uintptr_t pg = 4096;
+    const bool one_page = (((uintptr_t)slot & (pg - 1)) + sizeof(dpow_node_slot)) <= pg;
+    char *dev = nullptr;
     {
         std::lock_guard<std::mutex> g(g_page_mu);
         for (uintptr_t a = (uintptr_t)slot & ~(pg - 1); a < (uintptr_t)slot + sizeof(dpow_node_slot); a += pg) {
-            const hipError_t e = page_hold_locked(c, (void *)a);
+            char *d = nullptr;
+            const hipError_t e = page_hold_locked(c, (void *)a, &d);
             if (e != hipSuccess) return hip_fail(e, "dpow_node_attach: hipHostRegister");
+            if (!dev) dev = d;
         }
     }
-    void *d = nullptr;
-    DPOW_HIP(hipHostGetDevicePointer(&d, slot, 0));
+    void *d = dev + ((uintptr_t)slot & (pg - 1));
+    if (!one_page) DPOW_HIP(hipHostGetDevicePointer(&d, slot, 0));
     c->node = slot;
     c->d_node = (dpow_node_slot *)d;
     return 0;

@@ -13,7 +13,7 @@
 #                    `bench.py --gpus 8` (gloo, --same-device), the rocprofv3 kernel-trace and
 #                    PMC passes of the bench (tools/profile_gpu.sh)
 #   node [runs] [G,..] [small]   the emulated node alone
-#   node-small-ab name=lib.so ...   the emulated node's small cases per library (A/B of builds;
+#   node-small-ab name=lib.so[,VAR=value...] ...   the emulated node's small cases per library (A/B;
 #                    NODE_RUNS runs per case, default 3)
 #   timeline [G,..]  host timelines of one GPU's and the node ranks' searches (tools/owner_timeline.py)
 #   stl [G,..] [cases]   host + device timeline of small searches on one clock (tools/search_timeline.py)
@@ -73,8 +73,9 @@ node) timeout -k 10 600 python3 -u tools/node_probe.py "${1:-3}" "${2:-2,4,8}" $
 node-small-ab)  # the emulated 2/4/8-GPU node's small cases per library, twice, interleaved
     for rnd in 1 2; do
         for spec in "$@"; do
-            name=${spec%%=*}; lib=${spec#*=}
-            DPOW_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/node_probe.py ${NODE_RUNS:-3} 2,4,8 small \
+            name=${spec%%=*}; rest=${spec#*=}; lib=${rest%%,*}; envs=()
+            [ "$rest" != "$lib" ] && IFS=, read -ra envs <<< "${rest#*,}"
+            env "${envs[@]}" DPOW_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/node_probe.py ${NODE_RUNS:-3} 2,4,8 small \
                 > $out/node_${name}_$rnd.json 2> $out/node_${name}_$rnd.err || exit $?
         done
     done ;;

@@ -372,7 +372,7 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits,
     const auto dev = [share](uint64_t v) { return share > 1 && v > ~0ull / share ? ~0ull : v * (share ? share : 1); };
     const uint64_t expect = dev(expected_first_hit(ntz, rbits));
     const uint64_t eff = dev(candidates) < expect ? dev(candidates) : expect;
-    if (eff <= kTinyExpect) return kMaxBlocksPerCu < 2 ? kMaxBlocksPerCu : 2;
+    if (expect <= kTinyExpect || dev(candidates) <= kTinyLaunch) return kMaxBlocksPerCu < 2 ? kMaxBlocksPerCu : 2;
     if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
     if (eff <= kMidExpect) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
     if (kFiveExpect && expect <= kFiveExpect) return kMaxBlocksPerCu < 5 ? kMaxBlocksPerCu : 5;

@@ -137,7 +137,7 @@ constexpr uint32_t kNearPollWb = DPOW_NEAR_POLL_WB;
 constexpr uint64_t kFastPollCands = 1ull << 30;
 uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
 // Tiny searches -- a first hit expected within kTinyExpect candidates of the partition (N <= 5
-// on one GPU, N = 6 on a rank of an 8-GPU node): 2 workgroups per CU, claims of >= 2
+// on one GPU, N = 6 on a rank of a 2-, 4- or 8-GPU node): 2 workgroups per CU, claims of >= 2
 // wave-blocks, a poll of Ctrl::best after every wave-block.  There the launch's fixed cost
 // -- the waves' first chunks, the drain behind the hit -- outweighs its hashing: each wave
 // of a lightly loaded SIMD finishes a wave-block sooner.  Measured over the BASELINE cases
@@ -146,10 +146,16 @@ uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits);
 // [1,2,3,4]/6 0.043 -> 0.026 ms.  (Round 4 tried ending the tier at 2^20, moving an 8-GPU
 // rank's N = 6 to 3 workgroups per CU and claims of 4: the emulated node's [1,2,3,4]/6 went
 // 0.046 -> 0.056 ms, profiles/r04_small_probe/; not kept.)
+// Round 5: the tier reaches 2^23 expected (a 2-GPU rank's N = 6, a 4-GPU rank's 2^22); the
+// emulated node's G2 [1,2,3,4]/6 0.045 -> 0.038 ms (one GPU's 0.043: 0.93 -> 1.13x), G4 0.038
+// -> 0.034, nothing else moved (profiles/r05_ab.json[r05z_tiny/]).  A launch is tiny by its
+// size only up to kTinyLaunch (2^21, round 4's bound), so short windows of a search expected
+// late keep their grids.
 #ifndef DPOW_TINY_EXPECT_LOG2
-#define DPOW_TINY_EXPECT_LOG2 21
+#define DPOW_TINY_EXPECT_LOG2 23
 #endif
 constexpr uint64_t kTinyExpect = 1ull << DPOW_TINY_EXPECT_LOG2;
+constexpr uint64_t kTinyLaunch = 1ull << 21;
 // Up to kMidExpect (N = 6 on one GPU, N = 7 on a rank of a 4- or 8-GPU node): 4 workgroups
 // per CU.  The rate is ~6 % below the full grid's, but a rank that another rank's hit
 // stops drains in half the time: stop latency at N = 7 on an 8-GPU rank's window 103 ->

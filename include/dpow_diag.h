@@ -81,8 +81,9 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t n
 /* Worker workgroups per CU dpow_search gives a launch of `candidates` local indices
  * at (ntz, worker_bits) on a device it has alone (plan.cpp launch_blocks_per_cu): 6 (the
  * full persistent grid) unless the launch is short or a first hit is expected early
- * (16^ntz R / 256 candidates): 2 up to 2^21, 3 up to 2^22, 4 up to 2^26 candidates, and 5
- * while the hit is expected within 2^31. */
+ * (16^ntz R / 256 candidates): 2 for a hit expected within 2^23 (round 5; 2^21 before) or
+ * a launch of at most 2^21, else by the smaller of the two: 3 up to 2^22, 4 up to 2^26,
+ * and 5 while the hit is expected within 2^31. */
 uint64_t dpow_diag_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t worker_bits);
 
 /* Host timeline of the context's last dpow_search call, ns from its start (-1: did not

@@ -227,6 +227,8 @@ def test_grid_policy_for_short_launches():
     assert f(1 << 21, 32, 0) == 2 and f((1 << 21) + 1, 32, 0) == 3  # tiny launches (plan.h kTinyExpect)
     assert f(1 << 32, 6, 0) == 4 and f(1 << 32, 5, 0) == 2 and f(1 << 32, 7, 0) == 5  # 16^N expected
     assert f(1 << 32, 6, 3) == 2        # 16^6 * 32 / 256 = 2^21 candidates of a workerBits-3 partition
+    assert f(1 << 32, 6, 1) == 2 and f(1 << 32, 6, 2) == 2  # 2^23 / 2^22 expected: tiny since round 5
+    assert f(1 << 22, 32, 0) == 3 and f(1 << 23, 32, 0) == 4  # a short window expected late: by its size
     assert f(1 << 32, 7, 3) == 4 and f(1 << 32, 7, 2) == 4 and f(1 << 32, 7, 1) == 5  # 2^25 / 2^26 / 2^27
     # 5 per CU while a hit is expected within 2^31 candidates (plan.h kFiveExpect): an 8-GPU rank's
     # N = 8 (2^29); one GPU's N = 8 (2^32) and an 8-GPU rank's N = 9 (2^33) keep the full grid

@@ -1186,6 +1186,7 @@ int dpow_diag_vote_latency(uint32_t world, int reps, double *last_us, double *al
             pin(r);
             for (int rep = 1; rep <= reps; ++rep) {
                 while (go.load(std::memory_order_acquire) < rep) __builtin_ia32_pause();
+                if (failed.load()) break;  // rank 0 stopped: no rank waits for a vote that will not come
                 const int64_t in[3] = {(int64_t)(1000 + r), 1, 1};
                 int64_t out[3];
                 if (dpow_node_vote(votes, r, world, (uint64_t)rep, in, out, 1000000000) != 0) failed.store(1);
@@ -1204,7 +1205,8 @@ int dpow_diag_vote_latency(uint32_t world, int reps, double *last_us, double *al
     for (int rep = 1; rep <= reps && !failed.load(); ++rep) {
         go.store(rep, std::memory_order_release);
         for (uint32_t r = 1; r < world; ++r)
-            while (__atomic_load_n(&votes[2 * r + (rep & 1)].epoch, __ATOMIC_ACQUIRE) != (uint64_t)rep)
+            while (__atomic_load_n(&votes[2 * r + (rep & 1)].epoch, __ATOMIC_ACQUIRE) != (uint64_t)rep &&
+                   !failed.load())
                 __builtin_ia32_pause();
         for (const int64_t t_wait = now_ns(); now_ns() - t_wait < 2000;) __builtin_ia32_pause();
         const int64_t t0 = now_ns();
@@ -1213,9 +1215,10 @@ int dpow_diag_vote_latency(uint32_t world, int reps, double *last_us, double *al
         if (dpow_node_vote(votes, 0, world, (uint64_t)rep, in, out, 1000000000) != 0 || out[0] != 1000) failed.store(1);
         const int64_t t1 = now_ns();
         int64_t t_all = t1;
-        for (uint32_t r = 1; r < world; ++r) {
+        for (uint32_t r = 1; r < world && !failed.load(); ++r) {
             int64_t t;
-            while ((t = done_at[r].load(std::memory_order_acquire)) <= t_prev_done) __builtin_ia32_pause();
+            while ((t = done_at[r].load(std::memory_order_acquire)) <= t_prev_done && !failed.load())
+                __builtin_ia32_pause();
             t_all = std::max(t_all, t);
         }
         t_prev_done = t_all;

@@ -33,6 +33,7 @@
 #include "dpow_common.h"
 #include "md5_host.h"
 #include "md5_variants.h"
+#include "node.h"
 #include "plan.h"
 #include "../../include/dpow_diag.h"
 
@@ -946,6 +947,17 @@ void dpow_node_post(dpow_node_slot *slot, uint64_t global_idx) {
 
 int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, uint64_t epoch, const int64_t in[3],
                    int64_t out[3], int64_t timeout_ns) {
+    return dpow::node_vote(votes, rank, world, epoch, in, out, timeout_ns, nullptr);
+}
+
+}  // extern "C"
+
+// dpow_node_vote, and the wait of a board search (dpow_board_search): `abort_flag` non-NULL and
+// raised (the rank's cancel flag: its task was killed) ends the wait with DPOW_CANCELLED, the
+// vote left behind -- every rank of a board task is killed by the same Found / Cancel fan-out
+// (coordinator.go:210-230), so none is left waiting for it.
+int dpow::node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, uint64_t epoch, const int64_t in[3],
+                    int64_t out[3], int64_t timeout_ns, const uint32_t *abort_flag) {
     if (!votes || !in || !out || world == 0 || rank >= world || epoch == 0)
         return set_error(DPOW_EINVAL, "dpow_node_vote: bad argument");
     dpow_node_vote_entry &mine = votes[2 * rank + (epoch & 1)];
@@ -968,6 +980,7 @@ int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, u
         if (r == rank) continue;
         const dpow_node_vote_entry &e = votes[2 * r + (epoch & 1)];
         for (uint64_t it = 0; __atomic_load_n(&e.epoch, __ATOMIC_ACQUIRE) != epoch; ++it) {
+            if (abort_flag && it % 64 == 0 && __atomic_load_n(abort_flag, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
             if (it % 64 != 0 || now_ns() - t0 < std::min(kVoteSpinNs, timeout_ns)) {
                 __builtin_ia32_pause();
                 continue;
@@ -994,10 +1007,24 @@ int dpow_node_vote(dpow_node_vote_entry *votes, uint32_t rank, uint32_t world, u
     return 0;
 }
 
-int dpow_node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *votes, uint32_t rank, uint32_t world,
-                   uint64_t *epoch, int64_t vote_timeout_ns, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,
-                   uint64_t k_begin, uint64_t k_limit, uint64_t first_k, uint64_t batch_k, uint64_t *best_global_idx,
-                   uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len, uint32_t *batches) {
+extern "C" int dpow_node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *votes, uint32_t rank,
+                              uint32_t world, uint64_t *epoch, int64_t vote_timeout_ns, const uint8_t *nonce,
+                              size_t nonce_len, uint32_t ntz, uint64_t k_begin, uint64_t k_limit, uint64_t first_k,
+                              uint64_t batch_k, uint64_t *best_global_idx, uint8_t secret_out[DPOW_MAX_SECRET],
+                              size_t *secret_len, uint32_t *batches) {
+    return dpow::node_mine(c, slot, votes, rank, world, epoch, vote_timeout_ns, nonce, nonce_len, ntz, k_begin, k_limit,
+                           first_k, batch_k, best_global_idx, secret_out, secret_len, batches, false);
+}
+
+// dpow_node_mine; `abandon_on_cancel` (a board search, dpow_board_search): a rank whose cancel flag
+// is raised -- its task was killed by Found or Cancel -- stops the slot and returns DPOW_CANCELLED
+// at once instead of voting running = 0 and waiting for the other ranks' votes.  The fan-out kills
+// every rank of the task, so each leaves on its own kill, also when some rank never joined (a
+// worker that answered from its cache, worker.go:261-299).
+int dpow::node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *votes, uint32_t rank, uint32_t world,
+                    uint64_t *epoch, int64_t vote_timeout_ns, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,
+                    uint64_t k_begin, uint64_t k_limit, uint64_t first_k, uint64_t batch_k, uint64_t *best_global_idx,
+                    uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len, uint32_t *batches, bool abandon_on_cancel) {
     if (!c || !slot || !epoch || !best_global_idx || !secret_out || !secret_len || !batches)
         return set_error(DPOW_EINVAL, "dpow_node_mine: NULL argument");
     if (world == 0 || (world & (world - 1)) != 0 || world > 256 || rank >= world)
@@ -1037,8 +1064,20 @@ int dpow_node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *vote
         const uint64_t posted = __atomic_load_n(&slot->best, __ATOMIC_ACQUIRE);
         const int64_t in[3] = {(int64_t)(own < posted ? own : posted), running, err != 0 ? 0 : 1};
         int64_t out[3] = {in[0], in[1], in[2]};
+        if (abandon_on_cancel && err == 0 && __atomic_load_n(c->h_cancel, __ATOMIC_ACQUIRE) != 0u) {
+            // this rank was killed: leave without the vote
+            dpow_node_stop(slot);
+            status = DPOW_CANCELLED;
+            break;
+        }
         if (votes) {
-            const int vr = dpow_node_vote(votes, rank, world, ++*epoch, in, out, vote_timeout_ns);
+            const int vr = node_vote(votes, rank, world, ++*epoch, in, out, vote_timeout_ns,
+                                     abandon_on_cancel ? c->h_cancel : nullptr);
+            if (vr == DPOW_CANCELLED) {
+                dpow_node_stop(slot);
+                status = DPOW_CANCELLED;
+                break;
+            }
             if (vr < 0) {
                 err = err ? err : vr;
                 out[2] = 0;
@@ -1065,6 +1104,10 @@ int dpow_node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *vote
     if (status != DPOW_FOUND) *secret_len = 0;
     return status;
 }
+
+int dpow::fail(int code, const char *msg) { return set_error(code, msg); }
+
+extern "C" {
 
 int dpow_diag_node_post_at(dpow_node_slot *slot, uint64_t global_idx, int64_t t_ns) {
     if (!slot) return set_error(DPOW_EINVAL, "dpow_diag_node_post_at: slot is NULL");

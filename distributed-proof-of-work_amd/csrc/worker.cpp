@@ -3,7 +3,8 @@
 //   WorkerRPCHandler.Mine   worker.go:169-185  -> dpow_worker_mine
 //   WorkerRPCHandler.Cancel worker.go:189-198  -> dpow_worker_cancel
 //   WorkerRPCHandler.Found  worker.go:202-232  -> dpow_worker_found
-//   miner                   worker.go:258-401  -> Worker::miner (search loop = dpow_search windows)
+//   miner                   worker.go:258-401  -> Worker::miner (search loop = dpow_search windows, or
+//                                                 the node board's search, dpow_board_search)
 //   WorkerResultCache       worker.go:424-506  -> Worker::cache_get / cache_add
 //
 // A task's cancel channel (cap 1, worker.go:172) becomes a kill counter plus
@@ -89,6 +90,7 @@ struct CacheEntry {
 
 struct dpow_worker {
     int device = 0;
+    std::atomic<dpow_board *> board{nullptr};                // node mode (dpow_worker_set_board)
     std::mutex tasks_mu;                                    // WorkerMineTasks.mu
     std::map<std::string, std::shared_ptr<Task>> tasks;     // WorkerMineTasks.tasks
     std::mutex cache_mu;                                    // WorkerResultCache.mu
@@ -240,8 +242,25 @@ struct dpow_worker {
             if (t.kills > 0) *dpow_cancel_flag(ctx) = 1u;
         }
         int status = DPOW_EXHAUSTED;
+        bool own_hit = true;
+        dpow_board *const nb = board.load();
+        const bool node = nb && t.wbits >= 1 && t.wbits <= 6 && t.wb < (1u << t.wbits);
+        if (ctx && node) {
+            // The node's search of this task (dpow.h dpow_board_search): the deterministic first
+            // hit of all W partitions; reported by its owner only.
+            uint64_t best = DPOW_NO_HIT;
+            uint8_t sec[DPOW_MAX_SECRET];
+            size_t slen = 0;
+            uint32_t owner = 0;
+            status = dpow_board_search(nb, ctx, t.nonce.data(), t.nonce.size(), t.ntz, t.wb, t.wbits, &best, sec,
+                                       &slen, &owner);
+            if (status == DPOW_FOUND) {
+                secret.assign(sec, sec + slen);
+                own_hit = owner != 0;
+            }
+        }
         uint64_t k = 0, window = 1ull << 16;
-        while (ctx && status == DPOW_EXHAUSTED && k < DPOW_K_LIMIT) {  // worker.go:318-400
+        while (ctx && !node && status == DPOW_EXHAUSTED && k < DPOW_K_LIMIT) {  // worker.go:318-400
             const uint64_t ke = k + window < DPOW_K_LIMIT ? k + window : DPOW_K_LIMIT;
             uint64_t best = DPOW_NO_HIT;
             uint8_t sec[DPOW_MAX_SECRET];
@@ -275,7 +294,7 @@ struct dpow_worker {
             send(t.nonce, t.ntz, wb, nullptr, t.token, code);
             return;
         }
-        if (status == DPOW_FOUND) {  // worker.go:356-396
+        if (status == DPOW_FOUND && own_hit) {  // worker.go:356-396
             record(t.token, "WorkerResult", fields(t.nonce, t.ntz, &secret, &wb));
             send(t.nonce, t.ntz, wb, &secret, t.token);
             wait_kill(t);
@@ -285,7 +304,8 @@ struct dpow_worker {
         }
         // Killed while searching (worker.go:320-342).  A window exhausted up to
         // DPOW_K_LIMIT waits for the kill like the reference's never-ending
-        // loop would.
+        // loop would, and so does a node rank whose partition does not hold the node's
+        // first hit: the reference worker of that partition would still be searching.
         wait_kill(t);
         record(t.token, "WorkerCancel", fields(t.nonce, t.ntz, nullptr, &wb));
         send(t.nonce, t.ntz, wb, nullptr, t.token);
@@ -320,6 +340,12 @@ void dpow_worker_free(dpow_worker *w) {
         if (r.th.joinable()) r.th.join();
     for (dpow_ctx *c : w->pool) dpow_close(c);
     delete w;
+}
+
+int dpow_worker_set_board(dpow_worker *w, dpow_board *b) {
+    if (!w) return DPOW_EINVAL;
+    w->board.store(b);
+    return 0;
 }
 
 int dpow_worker_mine(dpow_worker *w, const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t worker_byte,

@@ -205,6 +205,15 @@ def lib():
         "dpow_node_mine": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, u64p, ctypes.c_int64,
                                           ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64,
                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, u8p, szp, u32p]),
+        "dpow_board_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(vp)]),
+        "dpow_board_close": (None, [vp]),
+        "dpow_board_unlink": (ctypes.c_int, [ctypes.c_char_p]),
+        "dpow_board_join": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+        "dpow_board_leave": (ctypes.c_int, [vp, vp]),
+        "dpow_board_tasks": (ctypes.c_int, [vp]),
+        "dpow_board_search": (ctypes.c_int, [vp, vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.c_uint32, u64p, u8p, szp, u32p]),
         "dpow_secret_from_index": (ctypes.c_int, [ctypes.c_uint64, u8p, szp]),
         "dpow_md5": (None, [ctypes.c_char_p, ctypes.c_size_t, u8p]),
         "dpow_trailing_zero_nibbles": (ctypes.c_uint32, [ctypes.c_char_p]),
@@ -247,6 +256,7 @@ def lib():
         "dpow_worker_next_result": (ctypes.c_int, [vp, ctypes.POINTER(WorkerResult), ctypes.c_int]),
         "dpow_worker_trace": (ctypes.c_size_t, [vp, ctypes.c_char_p, ctypes.c_size_t]),
         "dpow_worker_active_tasks": (ctypes.c_int, [vp]),
+        "dpow_worker_set_board": (ctypes.c_int, [vp, vp]),
     }
     missing = [name for name in sig if not hasattr(L, name)]
     if missing:  # same ABI version, yet entry points missing: not a library of this ABI either

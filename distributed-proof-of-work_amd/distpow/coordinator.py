@@ -13,6 +13,15 @@ round-robin on the node's GPUs, so the coordinator's workerBits fan-out
 Protocol kept: cache check; Mine fan-out; the first result wins (it must carry a
 secret); Found fan-out; wait for 2W messages in total; one extra Found round (W
 cache ACKs) per additional result; reply with the first result's secret.
+
+Node mode (the default for W a power of two in [2, 64]): the W workers share one node board
+(distpow.worker.Board, include/dpow.h dpow_board_*), so each task runs as one node search over
+the W partitions and only the owner of its minimum index reports it.  The first result is then
+the deterministic answer -- the reference enumeration's workerBits = 0 first hit -- instead of
+whichever worker happened to finish first; the messages are the reference's (2 per worker).
+The coordinator code below is the same in both modes: the change is entirely on the workers'
+side, as on a real node where each worker process opens the same board.  W = 1 and non-power-
+of-two W (coordinator.go:326 leaves overlapping partitions) keep first-arrived.
 Trace actions carry the reference's type names (CoordinatorMine,
 CoordinatorWorkerMine, CoordinatorWorkerResult, CoordinatorWorkerCancel,
 CoordinatorSuccess, CacheHit/Miss/Add/Remove).
@@ -23,7 +32,7 @@ import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
-from .worker import Worker
+from .worker import Board, Worker
 
 __all__ = ["Coordinator", "CoordinatorProtocolError"]
 
@@ -41,10 +50,18 @@ def _bytes_greater(a: bytes, b: bytes) -> bool:  # bytes.Compare(a, b) > 0
 
 
 class Coordinator:
-    def __init__(self, n_workers: int, devices: Sequence[int] = (0,), timeout_s: float = 600.0):
+    def __init__(self, n_workers: int, devices: Sequence[int] = (0,), timeout_s: float = 600.0,
+                 node: Optional[bool] = None):
         if n_workers < 1:
             raise ValueError("need at least one worker")
+        pow2 = 2 <= n_workers <= 64 and n_workers & (n_workers - 1) == 0
+        if node and not pow2:
+            raise ValueError("node mode needs W a power of two in [2, 64] (coordinator.go:326 partitions)")
         self.workers: List[Worker] = [Worker(devices[i % len(devices)]) for i in range(n_workers)]
+        self.board: Optional[Board] = Board() if (pow2 if node is None else node) else None
+        if self.board is not None:
+            for w in self.workers:
+                w.set_board(self.board)
         self.worker_bytes = [i & 0xFF for i in range(n_workers)]  # workerByte = uint8(i), coordinator.go:127
         self.worker_bits = int(math.log2(n_workers))              # uint(math.Log2(float64(W))), coordinator.go:326
         self.timeout_s = timeout_s
@@ -203,6 +220,9 @@ class Coordinator:
             t.join(timeout=5)
         for w in self.workers:
             w.close()
+        if self.board is not None:  # every miner has returned (Worker.close joins them)
+            self.board.close()
+            self.board = None
 
     def __enter__(self):
         return self

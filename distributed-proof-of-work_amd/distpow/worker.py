@@ -25,11 +25,61 @@ class WorkerResultWithToken:
     error: int = 0
 
 
+class Board:
+    """The node board (include/dpow.h dpow_board_*): the task entries through which the W
+    workers of one host run each task's node search, so the coordinator's first result is the
+    node's deterministic first hit.  name None: private to this process (the workers of one
+    process, e.g. the coordinator mirror); "/name": a POSIX shared-memory object every worker
+    process of the host opens."""
+
+    def __init__(self, name: Optional[str] = None):
+        self._b = ctypes.c_void_p()
+        self.name = name
+        check(lib().dpow_board_open(name.encode() if name else None, ctypes.byref(self._b)), "dpow_board_open")
+
+    @property
+    def handle(self):
+        return self._b
+
+    def tasks(self) -> int:
+        """Task entries in use (0 once every rank of every task has left)."""
+        return check(lib().dpow_board_tasks(self._b), "dpow_board_tasks")
+
+    def join(self, nonce, num_trailing_zeros, world, rank):
+        """(slot, votes) addresses of the task's entry for this rank (dpow_board_join)."""
+        n = bytes(nonce)
+        slot, votes = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().dpow_board_join(self._b, n, len(n), num_trailing_zeros, world, rank, ctypes.byref(slot),
+                                    ctypes.byref(votes)), "dpow_board_join")
+        return slot.value, votes.value
+
+    def leave(self, slot):
+        check(lib().dpow_board_leave(self._b, slot), "dpow_board_leave")
+
+    def close(self, unlink: bool = False):
+        if self._b:
+            lib().dpow_board_close(self._b)
+            self._b = ctypes.c_void_p()
+            if unlink and self.name:
+                check(lib().dpow_board_unlink(self.name.encode()), "dpow_board_unlink")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
 class Worker:
     def __init__(self, device: int = 0):
         self._w = ctypes.c_void_p()
         check(lib().dpow_worker_new(device, ctypes.byref(self._w)), "dpow_worker_new")
         self.device = device
+
+    def set_board(self, board: Optional[Board]):
+        """Node mode (dpow_worker_set_board): tasks with 1 <= workerBits <= 6 search on the board."""
+        check(lib().dpow_worker_set_board(self._w, board.handle if board is not None else None),
+              "dpow_worker_set_board")
 
     def close(self):
         if self._w:
@@ -80,4 +130,4 @@ class Worker:
         return lib().dpow_worker_active_tasks(self._w)
 
 
-__all__ = ["Worker", "WorkerResultWithToken", "DpowError"]
+__all__ = ["Board", "Worker", "WorkerResultWithToken", "DpowError"]

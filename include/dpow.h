@@ -30,9 +30,10 @@ extern "C" {
  * 7-byte chunks (round 2); dpow_node_* (round 3).
  * 3 (round 4): dpow_diag_launch_geometry takes ntz (dpow_diag.h); dpow_node_release.
  * 4 (round 5): dpow_node_mine.
+ * 5 (round 6): the node board, dpow_board_* (the node scheduler under the coordinator protocol).
  * A consumer built against another version must refuse the library before any
  * other call (distpow/_lib.py check_abi, tests/c/abi_harness.c). */
-#define DPOW_ABI_VERSION 4
+#define DPOW_ABI_VERSION 5
 
 /* "no hit" sentinel for global indices: INT64_MAX, so that signed (RCCL/gloo
  * int64 MIN) and unsigned (device atomicMin u64) reductions agree. */
@@ -196,6 +197,59 @@ int dpow_node_mine(dpow_ctx *ctx, dpow_node_slot *slot, dpow_node_vote_entry *vo
                    size_t nonce_len, uint32_t ntz, uint64_t k_begin, uint64_t k_limit, uint64_t first_k,
                    uint64_t batch_k, uint64_t *best_global_idx, uint8_t secret_out[DPOW_MAX_SECRET],
                    size_t *secret_len, uint32_t *batches);
+
+/* ---------------------------------------------------------------------------
+ * Node board (ABI 5): the node scheduler under the reference coordinator's unchanged protocol.
+ *
+ * The coordinator fans a task out to W workers, worker i searching prefix partition i
+ * (coordinator.go:122-129,179-199,326), and answers with the first result to arrive
+ * (coordinator.go:202).  When the W workers of a coordinator share one host (one worker per GPU
+ * of the node), they open one board, and each miner runs its partition's node search there
+ * (dpow_board_search): the task's entry -- keyed by (nonce, ntz, W), created by the first rank
+ * to arrive -- carries its node slot and votes, and every rank gets the node's first hit, the
+ * minimum global index over the partitions (the workerBits = 0 answer).  Only its owner reports
+ * it; the other workers wait for their kill (worker.go:320-342).  So the coordinator's first
+ * result is the deterministic answer, with the reference's messages unchanged: 2 per worker.
+ *
+ * Requirements: W a power of two in [2, DPOW_BOARD_MAX_WORLD]; all W workers of the
+ * coordinator on this host, sharing one board; one live task per (nonce, ntz) at a time (the
+ * reference's task maps, worker.go:173 and coordinator.go:175, key on the same).  A worker with
+ * W = 1 or a non-power-of-two W (coordinator.go:326 floor(log2 W) leaves partitions that
+ * overlap) searches alone with dpow_search, and the first result wins as in the reference.
+ * ------------------------------------------------------------------------- */
+#define DPOW_BOARD_MAX_WORLD 64
+#define DPOW_BOARD_TASKS 64      /* tasks in flight on one board at once */
+typedef struct dpow_board dpow_board;
+/* name NULL: a board private to this process (workers of one process, the coordinator mirror);
+ * else a POSIX shared-memory object "/name", created by the first worker process that opens it
+ * (zero-filled: an empty board) and mapped by every other. */
+int dpow_board_open(const char *name, dpow_board **out);
+/* Unmaps the board (no search may run on it); the shared object stays (dpow_board_unlink). */
+void dpow_board_close(dpow_board *b);
+int dpow_board_unlink(const char *name);
+/* Rank `rank` of `world` joins the task (nonce, ntz, world): its entry's slot and 2 * world vote
+ * entries (zeroed by the rank that created the entry).  dpow_board_leave: the last rank out
+ * frees the entry.  dpow_board_search does both; they are exposed for node schedulers that call
+ * dpow_node_mine themselves, and for tests. */
+int dpow_board_join(dpow_board *b, const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t world,
+                    uint32_t rank, dpow_node_slot **slot, dpow_node_vote_entry **votes);
+int dpow_board_leave(dpow_board *b, dpow_node_slot *slot);
+/* Task entries in use (0 once every joined rank has left). */
+int dpow_board_tasks(dpow_board *b);
+/* One worker's search of a task on the board: replaces the miner's loop (worker.go:301-400) when
+ * the node's W = 2^worker_bits workers share the board.  Joins the task's entry, runs
+ * dpow_node_mine for partition worker_byte (rank = worker_byte, world = 2^worker_bits) from k = 0,
+ * and leaves.  Returns DPOW_FOUND with *best_global_idx = the node's first hit and its secret;
+ * *owner = 1 when the hit lies in this worker's partition (this worker sends WorkerResult),
+ * 0 when another worker owns it (this worker waits for its kill, then sends the two nil
+ * messages of the cancel path).  DPOW_CANCELLED when the context's cancel flag is raised (the
+ * task's kill: Found or Cancel; the rank leaves at once, without waiting for the others' votes),
+ * or another rank's cancel stopped the task; a negative code when a search failed or another
+ * rank's did, or a vote timed out (120 s: a rank that never joined).  DPOW_EINVAL unless
+ * 1 <= worker_bits <= 6 and worker_byte < 2^worker_bits. */
+int dpow_board_search(dpow_board *b, dpow_ctx *ctx, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,
+                      uint32_t worker_byte, uint32_t worker_bits, uint64_t *best_global_idx,
+                      uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len, uint32_t *owner);
 
 /* ---------------------------------------------------------------------------
  * Host helpers (no GPU needed).

@@ -57,6 +57,15 @@ int dpow_worker_new(int device, dpow_worker **out);
 /* Cancels running miners, joins their threads, frees all resources. */
 void dpow_worker_free(dpow_worker *w);
 
+/* Node mode (ABI 5): the miners of this worker search on the node board `b` (dpow.h
+ * dpow_board_search) whenever the task's worker_bits is in [1, 6] and worker_byte <
+ * 2^worker_bits, so the node's W workers return the deterministic first hit through the
+ * unchanged protocol: the owner of the node's minimum index sends (result, nil ACK), every other
+ * worker (nil, nil) on its kill.  b = NULL turns node mode off.  Every worker of the coordinator
+ * must share the board (one process: one board; worker processes: dpow_board_open of one name);
+ * the board must outlive the worker's tasks.  Set it before the first Mine. */
+int dpow_worker_set_board(dpow_worker *w, dpow_board *b);
+
 /* WorkerRPCHandler.Mine (worker.go:169-185): register the task (key
  * hex(nonce)|ntz|workerByte), record WorkerMine, start the miner thread. */
 int dpow_worker_mine(dpow_worker *w, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,

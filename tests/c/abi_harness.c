@@ -77,6 +77,24 @@ int main(int argc, char **argv) {
     dpow_node_stop(&slot);
     if (slot.stop == 0 || dpow_node_attach(NULL, &slot) != DPOW_EINVAL) return fail("dpow_node_stop");
     if (dpow_search(NULL, nonce, 4, 6, 0, 0, 0, 1, NULL, secret, &len) != DPOW_EINVAL) return fail("NULL ctx");
+    /* the node board (ABI 5): two ranks of one task share an entry; the last one out frees it */
+    {
+        dpow_board *b = NULL;
+        dpow_node_slot *s0 = NULL, *s1 = NULL;
+        dpow_node_vote_entry *v0 = NULL, *v1 = NULL;
+        uint32_t owner = 9;
+        if (dpow_board_open(NULL, &b) != 0) return fail("dpow_board_open");
+        if (dpow_board_join(b, nonce, 4, 7, 4, 0, &s0, &v0) != 0 || dpow_board_join(b, nonce, 4, 7, 4, 3, &s1, &v1) != 0 ||
+            s0 != s1 || v0 != v1 || s0->best != DPOW_NO_HIT || dpow_board_tasks(b) != 1)
+            return fail("dpow_board_join");
+        if (dpow_board_leave(b, s0) != 0 || dpow_board_tasks(b) != 1 || dpow_board_leave(b, s1) != 0 ||
+            dpow_board_tasks(b) != 0 || dpow_board_leave(b, s1) != DPOW_EPROTO)
+            return fail("dpow_board_leave");
+        if (dpow_board_search(b, NULL, nonce, 4, 7, 0, 2, &slot.best, secret, &len, &owner) != DPOW_EINVAL ||
+            owner != 9)
+            return fail("dpow_board_search: NULL ctx");
+        dpow_board_close(b);
+    }
     if (sizeof(dpow_worker_result) != 56 + DPOW_MAX_NONCE) return fail("dpow_worker_result layout");
     const int gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
     /* The worker mirror as worker.go's RPC shell would drive it (include/dpow_worker.h). */

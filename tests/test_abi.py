@@ -49,7 +49,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_device_count():
     import distpow
     from distpow import _lib
-    assert distpow.lib().dpow_abi_version() == _lib.header_abi_version() == 4
+    assert distpow.lib().dpow_abi_version() == _lib.header_abi_version() == 5
     assert distpow.device_count() >= 0
 
 
@@ -90,7 +90,7 @@ def test_library_of_another_abi_is_refused(tmp_path):
 
 def test_library_missing_entry_points_is_refused(tmp_path):
     """The right version number but a missing entry point: refused too (no silent skip)."""
-    r = _load_in_child(_stub_library(tmp_path, 4, omit=("dpow_search_bound",)))
+    r = _load_in_child(_stub_library(tmp_path, 5, omit=("dpow_search_bound",)))
     assert r.returncode == 7, (r.stdout, r.stderr)
     assert "dpow_search_bound" in r.stdout
 
@@ -166,7 +166,7 @@ def test_c_abi_from_plain_c(tmp_path):
     distpow.lib()  # the build-id check
     out = subprocess.check_output([_build_c_harness(tmp_path)], timeout=60).decode()
     rec = json.loads(out)
-    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 4
+    assert rec["build_id"] == distpow.build_id() and rec["abi"] == 5
 
 
 @pytest.mark.gpu

@@ -1,0 +1,149 @@
+"""The node board's host logic (include/dpow.h dpow_board_*, csrc/board.cpp), no GPU needed.
+
+The board is what puts the node scheduler under the reference coordinator's protocol: the W
+workers of one host meet in one entry per task (coordinator.go:179-199 fans the task out;
+worker.go:173 keys it on nonce|ntz|workerByte), share its node slot and votes, and so agree on
+the node's minimum index.  Here: the entry matching rules, the last-one-out release, a full
+board, argument checks, and two processes sharing a named board (the shared-memory object each
+worker process of a node opens).
+"""
+import ctypes
+import multiprocessing as mp
+import os
+import uuid
+
+import pytest
+
+import distpow
+from distpow._lib import DPOW_NO_HIT, EINVAL, ENOMEM, EPROTO
+from distpow.worker import Board
+
+N1 = bytes([1, 2, 3, 4])
+
+
+def test_ranks_of_one_task_share_an_entry():
+    with Board() as b:
+        s0, v0 = b.join(N1, 7, 4, 0)
+        s3, v3 = b.join(N1, 7, 4, 3)
+        assert (s0, v0) == (s3, v3) and b.tasks() == 1
+        assert ctypes.c_uint64.from_address(s0).value == DPOW_NO_HIT  # a fresh slot
+        # another ntz, another world or another nonce is another task
+        assert b.join(N1, 8, 4, 0)[0] != s0
+        assert b.join(N1, 7, 8, 0)[0] != s0
+        assert b.join(bytes([2, 2, 2, 2]), 7, 4, 0)[0] != s0
+        assert b.tasks() == 4
+
+
+def test_a_rank_that_joined_already_starts_the_next_task():
+    """Rank 0 joining the same key again belongs to a later task with that key (its earlier
+    entry still holds ranks that have not left): a new entry, not the old one."""
+    with Board() as b:
+        s_a, _ = b.join(N1, 5, 2, 0)
+        s_b, _ = b.join(N1, 5, 2, 0)
+        assert s_a != s_b
+        # rank 1 of the first task joins the first entry (the oldest one it has not joined)
+        assert b.join(N1, 5, 2, 1)[0] == s_a
+
+
+def test_last_rank_out_frees_the_entry():
+    L = distpow.lib()
+    with Board() as b:
+        s, votes = b.join(N1, 6, 2, 0)
+        L.dpow_node_post(s, 1234)
+        b.join(N1, 6, 2, 1)
+        b.leave(s)
+        assert b.tasks() == 1
+        b.leave(s)
+        assert b.tasks() == 0
+        with pytest.raises(distpow.DpowError) as e:
+            b.leave(s)
+        assert e.value.code == EPROTO
+        # the freed entry is reset for its next task: fresh slot, zeroed votes
+        s2, v2 = b.join(N1, 6, 2, 0)
+        assert s2 == s and ctypes.c_uint64.from_address(s2).value == DPOW_NO_HIT
+        assert bytes((ctypes.c_uint8 * 256).from_address(v2)) == bytes(256)
+
+
+def test_a_task_some_ranks_never_join_is_freed_by_the_others():
+    """A worker that answers from its cache (worker.go:261-299) never joins: the entry goes
+    when the ranks that did join leave."""
+    with Board() as b:
+        s, _ = b.join(N1, 7, 4, 1)
+        b.join(N1, 7, 4, 2)
+        b.leave(s)
+        b.leave(s)
+        assert b.tasks() == 0
+
+
+def test_full_board_and_bad_arguments():
+    L = distpow.lib()
+    with Board() as b:
+        for i in range(64):  # DPOW_BOARD_TASKS
+            b.join(bytes([i]), 5, 2, 0)
+        with pytest.raises(distpow.DpowError) as e:
+            b.join(bytes([200]), 5, 2, 0)
+        assert e.value.code == ENOMEM
+        for world, rank in ((1, 0), (3, 0), (128, 0), (4, 4)):
+            with pytest.raises(distpow.DpowError) as e:
+                b.join(N1, 5, world, rank)
+            assert e.value.code == EINVAL
+        with pytest.raises(distpow.DpowError):
+            b.leave(12345)
+        best, slen, owner = ctypes.c_uint64(), ctypes.c_size_t(), ctypes.c_uint32(7)
+        sec = (ctypes.c_uint8 * 16)()
+        # no context: EINVAL, before any join
+        assert L.dpow_board_search(b.handle, None, N1, 4, 7, 0, 2, ctypes.byref(best), sec, ctypes.byref(slen),
+                                   ctypes.byref(owner)) == EINVAL
+        assert b.tasks() == 64
+
+
+def test_bad_names_are_refused():
+    for name in ("no_slash", "/a/b"):
+        with pytest.raises(distpow.DpowError):
+            Board(name)
+
+
+def _rank_proc(name, rank, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "distributed-proof-of-work_amd"))
+    import ctypes as ct
+
+    import distpow as dp
+    from distpow.worker import Board as B
+    try:
+        L = dp.lib()
+        b = B(name)
+        slot, votes = b.join(bytes([9, 9]), 6, 2, rank)
+        L.dpow_node_post(slot, 1000 + rank)  # atomic min into the shared slot
+        vin = (ct.c_int64 * 3)(100 + rank, 1, 1)
+        vout = (ct.c_int64 * 3)()
+        rc = L.dpow_node_vote(votes, rank, 2, 1, vin, vout, 30 * 10**9)
+        # after the vote both posts are in: the slot's best is the lower one
+        best = ct.c_uint64.from_address(slot).value
+        b.leave(slot)
+        q.put((rank, rc, list(vout), best))
+        b.close()
+    except Exception as e:  # reported to the parent
+        q.put((rank, "error", repr(e), None))
+
+
+def test_two_processes_share_a_named_board():
+    name = f"/dpow_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank_proc, args=(name, r, q)) for r in (0, 1)]
+    try:
+        for p in ps:
+            p.start()
+        out = sorted(q.get(timeout=240) for _ in ps)
+        for p in ps:
+            p.join(60)
+    finally:
+        distpow.lib().dpow_board_unlink(name.encode())
+    assert [o[1] for o in out] == [0, 0], out
+    assert [o[2] for o in out] == [[100, 1, 1], [100, 1, 1]]  # the same MIN on both ranks
+    assert [o[3] for o in out] == [1000, 1000]
+    with Board(name) as b:  # re-created empty after the unlink
+        assert b.tasks() == 0
+    distpow.lib().dpow_board_unlink(name.encode())

@@ -2,8 +2,11 @@
 
 BASELINE configs: 3 (4 workers, workerBits=2, N=7, cold then warm cache),
 4 (8 workers, workerBits=3, N=8), 5 (two concurrent clients, mixed nonces, 5..7 zeros).
-With W > 1 the reference's answer is whichever worker reports first; every
-returned secret must verify, and the message accounting must close (2W per task).
+With W a power of two the workers share a node board (node mode, csrc/board.cpp): the
+coordinator's first result is the node's first hit, so every answer is bit-exact with the
+reference enumeration's workerBits = 0 first hit (tests/golden/pow_golden.json), and the
+messages stay the reference's: 2 per worker, one WorkerResult per task (its owner's).
+Non-power-of-two W keeps first-arrived (coordinator.go:326): the secret must verify.
 """
 import hashlib
 import threading
@@ -11,46 +14,80 @@ import time
 
 import pytest
 
-import distpow
 from distpow.coordinator import Coordinator
 
 pytestmark = pytest.mark.gpu
+
+N1 = [1, 2, 3, 4]
 
 
 def ok(nonce, secret, n):
     return hashlib.md5(bytes(nonce) + bytes(secret)).hexdigest().endswith("0" * n)
 
 
+def golden_secret(golden, nonce, ntz):
+    for e in golden["first_hits"] + golden.get("deep_hits", []):
+        if e["nonce"] == list(nonce) and e["ntz"] == ntz:
+            return bytes(e["secret"]), e["global_idx"]
+    raise KeyError((nonce, ntz))
+
+
+def check_task_protocol(c, token, secret, g):
+    """One task through node mode: exactly one result (the owner's, workerByte = the owner of
+    the golden index g), each worker's actions in the reference's order (worker.go:177,363,
+    383 for the owner; 177,322 for a worker killed while it searches), and no message left
+    over (2W received, none dropped)."""
+    W = len(c.workers)
+    wbits = c.worker_bits
+    owner = (g & 255) >> (8 - wbits)
+    acts = [t for t in c.trace() if t["trace"] == token]
+    res = [t for t in acts if t["action"] == "CoordinatorWorkerResult"]
+    assert [(t["WorkerByte"], bytes(t["Secret"])) for t in res] == [(owner, secret)]
+    assert not [t for t in c.trace() if t["action"] == "CoordinatorDroppedResult"]
+    for w, wb in zip(c.workers, c.worker_bytes):
+        seq = [t["action"] for t in w.trace() if t["trace"] == token and
+               t["action"] in ("WorkerMine", "WorkerResult", "WorkerCancel")]
+        want = ["WorkerMine", "WorkerResult", "WorkerCancel"] if wb == owner else ["WorkerMine", "WorkerCancel"]
+        assert seq == want, (wb, seq)
+        assert w.active_tasks() == 0
+    assert c.board.tasks() == 0  # every rank left the task's entry
+
+
 def test_config3_four_workers_cold_then_warm(golden):
+    want, g = golden_secret(golden, N1, 7)
+    assert want == bytes([194, 170, 210, 13])
     with Coordinator(4) as c:
+        assert c.board is not None and c.worker_bits == 2
         t0 = time.perf_counter()
-        s = c.mine([1, 2, 3, 4], 7)
+        s = c.mine(N1, 7, token=101)
         cold = time.perf_counter() - t0
-        assert ok([1, 2, 3, 4], s, 7)
+        assert s == want  # the golden, not whichever worker finished first
+        check_task_protocol(c, 101, want, g)
         t0 = time.perf_counter()
-        s2 = c.mine([1, 2, 3, 4], 7)
+        s2 = c.mine(N1, 7)
         warm = time.perf_counter() - t0
-        # warm: the coordinator cache may hold a lexicographically larger secret of a later worker
-        assert ok([1, 2, 3, 4], s2, 7) and c.cache_entry([1, 2, 3, 4])[1] == s2
+        assert s2 == want and c.cache_entry(N1) == (7, want)
         acts = [t["action"] for t in c.trace()]
         assert acts.count("CoordinatorWorkerMine") == 4
         assert acts[-3:] == ["CoordinatorMine", "CacheHit", "CoordinatorSuccess"]
         # lower N is a cache hit too (cached N >= requested)
-        assert c.mine([1, 2, 3, 4], 5) == s2
+        assert c.mine(N1, 5) == want
         print(f"config3 cold {cold * 1e3:.1f} ms warm {warm * 1e3:.3f} ms secret {list(s)}")
 
 
 def test_config4_eight_workers_n8(golden):
     with Coordinator(8) as c:
         assert c.worker_bits == 3
-        s = c.mine([1, 2, 3, 4], 8)
-        assert ok([1, 2, 3, 4], s, 8)
-        s = c.mine([2, 2, 2, 2], 8)
-        assert ok([2, 2, 2, 2], s, 8)
+        for tok, nonce in ((201, N1), (202, [2, 2, 2, 2])):
+            want, g = golden_secret(golden, nonce, 8)
+            assert c.mine(nonce, 8, token=tok) == want
+            check_task_protocol(c, tok, want, g)
+    assert golden_secret(golden, N1, 8)[0] == bytes([10, 189, 80, 242])
+    assert golden_secret(golden, [2, 2, 2, 2], 8)[0] == bytes([218, 55, 128, 17])
 
 
-def test_config5_two_concurrent_clients():
-    reqs = [([1, 2, 3, 4], 7), ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5), ([2, 2, 2, 2], 7)]
+def test_config5_two_concurrent_clients(golden):
+    reqs = [(N1, 7), ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5), ([2, 2, 2, 2], 7)]
     with Coordinator(4) as c:
         out = {}
 
@@ -63,14 +100,53 @@ def test_config5_two_concurrent_clients():
         a.start(); b.start(); a.join(120); b.join(120)
         assert len(out) == 4
         for (i, nonce, n), s in out.items():
-            assert ok(list(nonce), s, n)
-        # the later [2,2,2,2]/7 request (or its cache) dominates the /5 entry
-        assert c.cache_entry([2, 2, 2, 2])[0] >= 7
+            assert s == golden_secret(golden, nonce, n)[0], (nonce, n, list(s))
+        assert out[(0, (5, 6, 7, 8), 5)] == bytes([84, 244, 3])
+        # the later [2,2,2,2]/7 request dominates the /5 entry (coordinator.go:455-470)
+        assert c.cache_entry([2, 2, 2, 2]) == (7, bytes([218, 55, 128, 17]))
+        assert not [t for t in c.trace() if t["action"] == "CoordinatorDroppedResult"]
+        assert c.board.tasks() == 0
+
+
+def test_worker_cache_hit_in_node_mode(golden):
+    """A worker answering from its cache (worker.go:261-299) never joins the task's entry; the
+    other workers leave it on their kill, and the 2W messages still close."""
+    want, _ = golden_secret(golden, N1, 6)
+    with Coordinator(4) as c:
+        # seed worker 2's cache only, as if it alone had served the nonce before; its Found ACK
+        # reaches the coordinator outside any request (dropped, coordinator.go:318)
+        c.workers[2].found(N1, 6, 2, want, 300)
+        deadline = time.time() + 10
+        while not [t for t in c.trace() if t["trace"] == 300] and time.time() < deadline:
+            time.sleep(0.01)
+        s = c.mine(N1, 6, token=301)
+        assert s == want
+        res = [t for t in c.trace() if t["trace"] == 301 and t["action"] == "CoordinatorWorkerResult"]
+        assert [(t["WorkerByte"], bytes(t["Secret"])) for t in res] == [(2, want)]
+        assert not [t for t in c.trace() if t["trace"] == 301 and t["action"] == "CoordinatorDroppedResult"]
+        for w, wb in zip(c.workers, c.worker_bytes):
+            seq = [t["action"] for t in w.trace() if t["trace"] == 301 and
+                   t["action"] in ("WorkerMine", "CacheHit", "WorkerResult", "WorkerCancel")]
+            want_seq = (["WorkerMine", "CacheHit", "WorkerResult", "WorkerCancel"] if wb == 2
+                        else ["WorkerMine", "WorkerCancel"])
+            assert seq == want_seq, (wb, seq)
+        deadline = time.time() + 10
+        while c.board.tasks() and time.time() < deadline:
+            time.sleep(0.01)
+        assert c.board.tasks() == 0
+
+
+def test_first_arrived_mode_still_verifies():
+    """node=False: the reference's race (coordinator.go:202), every answer verified."""
+    with Coordinator(4, node=False) as c:
+        assert c.board is None
+        s = c.mine([9, 9, 9, 9], 5)
+        assert ok([9, 9, 9, 9], s, 5)
 
 
 def test_non_power_of_two_workers_quirk():
     """coordinator.go:326 floor(log2 3) = 1: worker 2's prefix (2 << 7) wraps onto worker 0's."""
     with Coordinator(3) as c:
-        assert c.worker_bits == 1
+        assert c.worker_bits == 1 and c.board is None
         s = c.mine([9, 9, 9, 9], 4)
         assert ok([9, 9, 9, 9], s, 4)

@@ -714,35 +714,60 @@ def node_devices(world, same_device, visible):
     return [0] * world if same_device else [i % n for i in range(world)]
 
 
+# The reference enumeration's first hits (worker.go:301-400 at workerBits = 0) of the coordinator
+# requests below: tests/golden/pow_golden.json first_hits.  In node mode the coordinator's answer
+# must be exactly these.
+COORD_GOLDEN = {((1, 2, 3, 4), 7): 231910082, ((1, 2, 3, 4), 8): 4065377546, ((5, 6, 7, 8), 5): 259156,
+                ((2, 2, 2, 2), 5): 30512, ((2, 2, 2, 2), 7): 293615578, ((2, 2, 2, 2), 8): 293615578}
+
+
 def coordinator_configs(devices=(0,)):
     """BASELINE configs 3-5 end to end through the coordinator mirror (coordinator.go:139-320)
     over native workers (worker.go:169-232), logical worker i on devices[i % len(devices)] (one
-    GPU: all of them on this rank's): wall ms per client request, first-arrived answers as the
-    reference gives them, each verified."""
+    GPU: all of them on this rank's).  The workers share a node board (W a power of two), so each
+    answer is the node's first hit: `answers` gives its global index and whether it is the golden
+    (COORD_GOLDEN); a wrong one fails the section.  Times are wall ms per client request."""
     import threading
     from distpow.coordinator import Coordinator
 
-    def timed(c, nonce, n):
+    answers = {}
+
+    def timed(c, nonce, n, name=None):
         t = time.perf_counter()
         s = c.mine(nonce, n)
+        ms = round((time.perf_counter() - t) * 1e3, 3)
         if not distpow.verify(nonce, s, n):
             raise RuntimeError(f"coordinator: {bytes(nonce).hex()}/{n} returned {list(s)}, which does not verify")
-        return round((time.perf_counter() - t) * 1e3, 3)
+        if name:
+            g = distpow.global_index(int.from_bytes(s[1:], "little"), s[0])  # secret = threadByte || chunk_k
+            want = COORD_GOLDEN.get((tuple(nonce), n))
+            answers[name] = {"global_idx": g, "golden": g == want}
+            if want is not None and g != want:
+                answers[name]["ok"] = False
+        return ms
 
     devices = list(devices)
     out = {"devices": devices} if len(devices) > 1 else {}
-    with Coordinator(4, devices) as c:  # config 3: 4 workers (workerBits = 2), N = 7, cold then warm cache
-        out["config3_4workers_n7_cold_ms"] = timed(c, [1, 2, 3, 4], 7)
-        out["config3_4workers_n7_warm_ms"] = timed(c, [1, 2, 3, 4], 7)
+    cold = []
+    for rep in range(3):  # config 3: 4 workers (workerBits = 2), N = 7, cold then warm cache
+        with Coordinator(4, devices) as c:
+            if rep == 0:
+                out["mode"] = "node board" if c.board is not None else "first-arrived"
+            cold.append(timed(c, [1, 2, 3, 4], 7, "config3_n7" if rep == 0 else None))
+            if rep == 0:
+                out["config3_4workers_n7_warm_ms"] = timed(c, [1, 2, 3, 4], 7)
+    out["config3_4workers_n7_cold_ms"] = cold[0]
+    out["config3_4workers_n7_cold_median_ms"] = sorted(cold)[1]
     with Coordinator(8, devices) as c:  # config 4: 8 workers (workerBits = 3), N = 8
-        out["config4_8workers_n8_ms"] = timed(c, [1, 2, 3, 4], 8)
+        out["config4_8workers_n8_ms"] = timed(c, [1, 2, 3, 4], 8, "config4_n8")
+        out["config4_8workers_n8_nonce2222_ms"] = timed(c, [2, 2, 2, 2], 8, "config4_n8_nonce2222")
     with Coordinator(4, devices) as c:  # config 5: two concurrent clients (cmd/client/main.go:40-51)
         reqs = [([1, 2, 3, 4], 7), ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5), ([2, 2, 2, 2], 7)]
         done = {}
 
         def client(i, items):
             for nonce, n in items:
-                done[(i, n, bytes(nonce))] = timed(c, nonce, n)
+                done[(i, n, bytes(nonce))] = timed(c, nonce, n, f"config5_{bytes(nonce).hex()}_n{n}")
 
         t = time.perf_counter()
         th = [threading.Thread(target=client, args=(0, reqs[:2])), threading.Thread(target=client, args=(1, reqs[2:]))]
@@ -753,8 +778,9 @@ def coordinator_configs(devices=(0,)):
         if len(done) != 4:
             raise RuntimeError(f"config 5: {len(done)} of 4 client requests finished within 120 s")
         out["config5_two_clients_total_ms"] = round((time.perf_counter() - t) * 1e3, 3)
-    # Config 4's one nonce times one draw (which worker holds the first hit, and the share of the
-    # device its search got); over fresh nonces the mean follows the device's aggregate rate.
+    out["answers"] = answers
+    # Config 4's one nonce times one draw (where the node's first hit lies); over fresh nonces the
+    # mean follows the device's aggregate rate.
     import random
     rng = random.Random(20261017)
     with Coordinator(8, devices) as c:

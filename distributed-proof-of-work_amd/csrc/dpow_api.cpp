@@ -675,46 +675,59 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
 // unregistered under a running watcher.  Memory about to be unmapped is released explicitly
 // (dpow_node_release: NodeBoard.close), so a new mapping at the same address is registered
 // afresh instead of reusing the old registration's device alias.
+// The registration is portable (every device of the process may map the page) and the device
+// alias is looked up per device, under that device, the first time a context of that device
+// holds the page: a process whose contexts on several GPUs share one slot (a node scheduler with
+// a context per GPU, the board's workers) never hands one GPU's alias to another's watcher
+// (VERDICT r05 item 2(i)).
 struct PageEntry {
     void *page;
     bool foreign;                    // registered outside this library: never unregistered here
     std::vector<dpow_ctx *> holders;
-    char *dev = nullptr;             // the page's device alias (hipHostGetDevicePointer, once)
+    char *dev[kMaxDevices] = {};     // the page's alias on each device (hipHostGetDevicePointer, once per device)
 };
 std::mutex g_page_mu;
 std::vector<PageEntry> g_pages;
-
-// A reference of ctx on `page` (registering it if no context holds it).  g_page_mu held.
-// *dev: the page's device alias.
-hipError_t page_hold_locked(dpow_ctx *c, void *page, char **dev) {
-    for (PageEntry &pe : g_pages)
-        if (pe.page == page) {
-            if (std::find(pe.holders.begin(), pe.holders.end(), c) == pe.holders.end()) pe.holders.push_back(c);
-            *dev = pe.dev;
-            return hipSuccess;
-        }
-    hipError_t e = hipHostRegister(page, 4096, hipHostRegisterMapped);
-    bool foreign = false;
-    if (e == hipErrorHostMemoryAlreadyRegistered) {
-        (void)hipGetLastError();
-        e = hipSuccess;
-        foreign = true;
-    }
-    if (e != hipSuccess) return e;
-    void *d = nullptr;
-    if ((e = hipHostGetDevicePointer(&d, page, 0)) != hipSuccess) {
-        if (!foreign) (void)hipHostUnregister(page);
-        return e;
-    }
-    g_pages.push_back(PageEntry{page, foreign, {c}, static_cast<char *>(d)});
-    *dev = static_cast<char *>(d);
-    return hipSuccess;
-}
 
 // Drop entry i (every holder's streams drained by the caller).  g_page_mu held.
 void page_drop_locked(size_t i) {
     if (!g_pages[i].foreign) (void)hipHostUnregister(g_pages[i].page);
     g_pages.erase(g_pages.begin() + (long)i);
+}
+
+// A reference of ctx on `page` (registering it if no context holds it).  g_page_mu held, the
+// calling thread on ctx's device.  *dev: the page's alias on ctx's device.
+hipError_t page_hold_locked(dpow_ctx *c, void *page, char **dev) {
+    PageEntry *pe = nullptr;
+    for (PageEntry &x : g_pages)
+        if (x.page == page) {
+            pe = &x;
+            break;
+        }
+    if (!pe) {
+        hipError_t e = hipHostRegister(page, 4096, hipHostRegisterMapped | hipHostRegisterPortable);
+        bool foreign = false;
+        if (e == hipErrorHostMemoryAlreadyRegistered) {
+            (void)hipGetLastError();
+            e = hipSuccess;
+            foreign = true;
+        }
+        if (e != hipSuccess) return e;
+        g_pages.push_back(PageEntry{page, foreign, {}, {}});
+        pe = &g_pages.back();
+    }
+    if (!pe->dev[c->device]) {
+        void *d = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&d, page, 0);
+        if (e != hipSuccess) {
+            if (pe->holders.empty()) page_drop_locked((size_t)(pe - g_pages.data()));
+            return e;
+        }
+        pe->dev[c->device] = static_cast<char *>(d);
+    }
+    if (std::find(pe->holders.begin(), pe->holders.end(), c) == pe->holders.end()) pe->holders.push_back(c);
+    *dev = pe->dev[c->device];
+    return hipSuccess;
 }
 
 // dpow_close: ctx's references go (its stream has drained); pages without holders are unregistered.
@@ -879,6 +892,7 @@ int dpow_node_attach(dpow_ctx *c, dpow_node_slot *slot) {
         return 0;
     }
     if (((uintptr_t)slot & 7u) != 0u) return set_error(DPOW_EINVAL, "dpow_node_attach: slot not 8-byte aligned");
+    if (c->device >= kMaxDevices) return set_error(DPOW_EINVAL, "dpow_node_attach: device ordinal too large");
     // Map the slot's host page(s) for the watcher (fine-grained: hipHostRegister's default).
     const DeviceScope on_device(c->device);
     if (on_device.e != hipSuccess) return hip_fail(on_device.e, "hipSetDevice");
@@ -1375,6 +1389,16 @@ int dpow_diag_launch_geometry(const uint8_t *nonce, size_t nonce_len, uint32_t n
         ++n;
     }
     return (int)n;
+}
+
+int dpow_diag_node_alias(dpow_ctx *c, void **cached, void **lookup) {
+    if (!c || !cached || !lookup) return set_error(DPOW_EINVAL, "dpow_diag_node_alias: NULL argument");
+    if (!c->node) return set_error(DPOW_EINVAL, "dpow_diag_node_alias: no slot attached");
+    const DeviceScope on_device(c->device);
+    if (on_device.e != hipSuccess) return hip_fail(on_device.e, "hipSetDevice");
+    *cached = c->d_node;
+    DPOW_HIP(hipHostGetDevicePointer(lookup, c->node, 0));
+    return 0;
 }
 
 int dpow_diag_search_times(dpow_ctx *c, int64_t out[8]) {

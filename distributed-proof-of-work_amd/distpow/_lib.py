@@ -240,6 +240,7 @@ def lib():
         "dpow_diag_blocks_per_cu": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
         "dpow_diag_search_times": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "dpow_diag_node_post_at": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_int64]),
+        "dpow_diag_node_alias": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         "dpow_diag_search_launches": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(LaunchTime),
                                                      ctypes.c_size_t]),
         "dpow_diag_clock_sync": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),

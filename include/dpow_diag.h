@@ -139,6 +139,12 @@ int dpow_diag_vote_latency(uint32_t world, int reps, double *last_us, double *al
  * Returns 0, or < 0 on error. */
 int dpow_diag_node_post_at(struct dpow_node_slot *slot, uint64_t global_idx, int64_t t_ns);
 
+/* The device alias of the slot attached to ctx, as its watcher reads it (*cached: from the page
+ * registry), and as hipHostGetDevicePointer gives it now under ctx's device (*lookup).  They
+ * must agree for every context of a process, whatever device registered the page first
+ * (round 6: the registry keeps one alias per device).  DPOW_EINVAL when no slot is attached. */
+int dpow_diag_node_alias(struct dpow_ctx *ctx, void **cached, void **lookup);
+
 #ifdef __cplusplus
 }
 #endif

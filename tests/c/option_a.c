@@ -26,7 +26,7 @@
  * returned: its "reuse" scenario must report the late kill cancelling the pooled context's
  * next search (exit 5).
  *
- * Scenarios (argv[2..], default all): late_found, early_found, race, cancel, reuse, fanout.
+ * Scenarios (argv[2..], default all): late_found, early_found, race, cancel, reuse, fanout, fanout_node.
  * Exit 0 and one JSON line on success; 4 on a missing message (deadlock), 5 on a protocol
  * violation (a third message, a wrong order, a wrong secret, a leaked goroutine or context).
  */
@@ -37,6 +37,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "dpow.h"
 
@@ -213,6 +214,9 @@ static int results_recv(msg *out, double timeout_s) { /* 0, or -1 on timeout */
  * tests/test_option_a.py checks that the two stay line for line the same flow ("..." in a
  * quote stands for the rest of a long Go line). */
 static int g_device;
+/* gpuBoard: opened by the binding's init() from DPOW_NODE_BOARD; here by the
+ * fanout_node scenario (a named board, as the W worker processes of a node would open it). */
+static dpow_board *g_board;
 static struct {
     dpow_ctx *free[64];
     int n, cap;         /* go: var gpuCtxs = ctxPool{free: make(chan *C.dpow_ctx, gpuPoolSize)} */
@@ -316,6 +320,27 @@ static uint8_t *gpu_search(task *t, size_t *len, search_state **killed) { /* go:
     uint8_t sec[DPOW_MAX_SECRET];                                         /* go: var sec [C.DPOW_MAX_SECRET]C.uint8_t */
     size_t slen = 0;                                                      /* go: var slen C.size_t */
     uint8_t *secret = NULL;
+    if (g_board != NULL && t->worker_bits >= 1 && t->worker_bits <= 6 &&
+        t->worker_byte < (1u << t->worker_bits)) {                        /* go: if gpuBoard != nil && args.WorkerBits >= 1 && ... */
+        uint64_t best = 0;                                                /* go: var best C.uint64_t */
+        uint32_t owner = 0;                                               /* go: var owner C.uint32_t */
+        const int rc = dpow_board_search(g_board, ctx, nonce, t->nonce_len, t->ntz, t->worker_byte,
+                                         t->worker_bits, &best, sec, &slen, &owner); /* go: rc := C.dpow_board_search(gpuBoard, ctx, ... */
+                                                                          /* go: switch { */
+        if (rc == DPOW_FOUND && owner != 0) {                             /* go: case rc == C.DPOW_FOUND && owner != 0: */
+            secret = malloc(slen);                                        /* go: return C.GoBytes(unsafe.Pointer(&sec[0]), C.int(slen)), k */
+            memcpy(secret, sec, slen);
+            *len = slen;
+            goto out;
+        }
+        if (rc == DPOW_FOUND || rc == DPOW_CANCELLED) {                   /* go: case rc == C.DPOW_FOUND || rc == C.DPOW_CANCELLED: */
+            chan_recv(&s->k);                                             /* go: <-k */
+            goto out;                                                     /* go: return nil, k */
+        }
+                                                                          /* go: default: */
+        fprintf(stderr, "option_a: dpow_board_search: %d (%s)\n", rc, dpow_last_error());
+        abort();                                                          /* go: panic(C.GoString(C.dpow_last_error())) */
+    }
     uint64_t window = 1u << 16;                                           /* go: window := uint64(1 << 16) */
     for (uint64_t k_begin = 0; k_begin < DPOW_K_LIMIT;) {                 /* go: for kBegin := uint64(0); kBegin < C.DPOW_K_LIMIT; { */
         uint64_t k_end = k_begin + window;                                /* go: kEnd := kBegin + window */
@@ -627,6 +652,49 @@ static void sc_fanout(int *results) {
     (*results)++; /* the first one */
 }
 
+/* The same fan-out with the W workers on a node board (DPOW_NODE_BOARD, dpow.h
+ * dpow_board_search): the first result is the node's first hit -- the golden, reported by the
+ * owner of its index only -- and the other workers send their two nil messages on the kill. */
+static void sc_fanout_node(void) {
+    const char *sc = "fanout_node";
+    const int W = 4;
+    const uint32_t n = g_fake ? 4 : 7;
+    const uint64_t golden = g_fake ? 5236u : 231910082u; /* tests/golden/pow_golden.json first_hits */
+    const int owner = (int)((golden & 255u) >> 6);
+    char name[64];
+    snprintf(name, sizeof name, "/dpow_option_a_%ld", (long)getpid());
+    if (dpow_board_open(name, &g_board) != 0) die(5, sc, "dpow_board_open");
+    task *t[4];
+    for (int i = 0; i < W; i++) t[i] = new_task(N1234, 4, n, (uint32_t)i, 2);
+    for (int i = 0; i < W; i++) rpc_mine(t[i]);
+    msg m;
+    if (results_recv(&m, g_timeout_s) != 0) die(4, sc, "no first result");
+    if (!m.has_secret) die(5, sc, "first message is not a result");
+    if (m.task != t[owner]->id) die(5, sc, "the first result is not the owner's");
+    if (!is_secret(&m, golden)) die(5, sc, "the first result is not the node's first hit (the golden)");
+    int count[4] = {0}, got = 1;
+    count[owner] = 1;
+    for (int i = 0; i < W; i++) rpc_found(t[i]); /* coordinator.go:210-230 */
+    while (got < 2 * W) {                         /* coordinator.go:237-248 */
+        if (results_recv(&m, g_timeout_s) != 0) die(4, sc, "fewer than 2W messages");
+        const int i = m.task - t[0]->id;
+        if (i < 0 || i >= W) die(5, sc, "a message of another task");
+        if (m.has_secret) die(5, sc, "a second result (only the owner reports)");
+        count[i]++;
+        got++;
+    }
+    for (int i = 0; i < W; i++) {
+        if (count[i] != 2) die(5, sc, "a worker did not send exactly 2 messages");
+        if (i == owner) expect_trace(sc, t[i], ACT_MINE, ACT_RESULT, ACT_CANCEL);
+        else expect_trace(sc, t[i], ACT_MINE, ACT_CANCEL, 0);
+    }
+    expect_quiet(sc, 0.1);
+    if (dpow_board_tasks(g_board) != 0) die(5, sc, "a rank did not leave the task's board entry");
+    dpow_board_close(g_board);
+    g_board = NULL;
+    dpow_board_unlink(name);
+}
+
 int main(int argc, char **argv) {
     if (dpow_abi_version() != DPOW_ABI_VERSION) { /* the binding's init() */
         fprintf(stderr, "option_a: libdpow.so implements ABI %d, built for %d\n", dpow_abi_version(),
@@ -641,12 +709,12 @@ int main(int argc, char **argv) {
     if (g_fake) g_timeout_s = 60.0;
     const char *to = getenv("OPTION_A_TIMEOUT_S"); /* how long a missing message is waited for */
     if (to && atof(to) > 0) g_timeout_s = atof(to);
-    int want[6] = {1, 1, 1, 1, 1, 1};
-    static const char *names[6] = {"late_found", "early_found", "race", "cancel", "reuse", "fanout"};
+    int want[7] = {1, 1, 1, 1, 1, 1, 1};
+    static const char *names[7] = {"late_found", "early_found", "race", "cancel", "reuse", "fanout", "fanout_node"};
     if (argc > 2) {
         memset(want, 0, sizeof want);
         for (int a = 2; a < argc; a++)
-            for (int i = 0; i < 6; i++)
+            for (int i = 0; i < 7; i++)
                 if (strcmp(argv[a], names[i]) == 0) want[i] = 1;
     }
     const double t0 = now_s();
@@ -659,6 +727,7 @@ int main(int argc, char **argv) {
     if (want[3]) sc_cancel(&cancel_ms);
     if (want[4]) sc_reuse();
     if (want[5]) sc_fanout(&fanout_results);
+    if (want[6]) sc_fanout_node();
     /* every goroutine has exited: each got its kill (none is left waiting on a killChan) */
     const double dl = now_s() + 10.0;
     pthread_mutex_lock(&g_mu);
@@ -679,7 +748,7 @@ int main(int argc, char **argv) {
     if (g_pool.opens != g_pool.closes) die(5, "teardown", "a context leaked");
     printf("{\"ok\": true, \"mode\": \"%s\", \"flow\": \"%s\", \"goroutines\": %d, \"contexts_opened\": %d, "
            "\"contexts_closed\": %d, \"early_found_cancelled\": %d, \"race_reps\": %d, \"race_results\": %d, "
-           "\"cancel_latency_ms\": %.3f, \"fanout_results\": %d, \"seconds\": %.3f}\n",
+           "\"cancel_latency_ms\": %.3f, \"fanout_results\": %d, \"fanout_node\": %s, \"seconds\": %.3f}\n",
            g_fake ? "fake" : "gpu",
 #if defined(OPTION_A_R04)
            "r04",
@@ -689,6 +758,6 @@ int main(int argc, char **argv) {
            "r05",
 #endif
            nth, g_pool.opens, g_pool.closes, early_cancelled, want[2] ? race_reps : 0, race_results, cancel_ms,
-           fanout_results, now_s() - t0);
+           fanout_results, want[6] ? "true" : "false", now_s() - t0);
     return 0;
 }

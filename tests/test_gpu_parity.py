@@ -712,13 +712,21 @@ def test_two_contexts_share_a_slot_one_closes(miner, golden):
     addr = ctypes.addressof(slot)
     lib = distpow.lib()
     lib.dpow_node_slot_reset(addr)
-    other = distpow.Miner(0)
+    other = distpow.Miner(distpow.device_count() - 1)  # another GPU when the box has one
     try:
         other.attach_node(addr)
         miner.attach_node(addr)
+        # each context's watcher reads the slot through its own device's alias
+        for m in (other, miner):
+            cached, lookup = ctypes.c_void_p(), ctypes.c_void_p()
+            assert lib.dpow_diag_node_alias(m._ctx, ctypes.byref(cached), ctypes.byref(lookup)) == 0
+            assert cached.value == lookup.value and cached.value
         assert other.search([1, 2, 3, 4], 3, 0, 0, 0, 1 << 10).status == FOUND  # other's launches used the page
     finally:
         other.close()  # drops other's hold; the miner's keeps the page registered
+    cached, lookup = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.dpow_diag_node_alias(miner._ctx, ctypes.byref(cached), ctypes.byref(lookup)) == 0
+    assert cached.value == lookup.value
     try:
         assert _stopped_by_node(miner, lib, addr) < 0.25
         # the node's best through the page: a bound below the answer leaves nothing to find

@@ -53,6 +53,7 @@ def test_option_a_flow_on_cpu(tmp_path):
     assert rec["contexts_opened"] == rec["contexts_closed"] >= 1
     assert rec["early_found_cancelled"] == 1  # the Found stopped a 2.5 M-candidate search
     assert rec["race_reps"] == 24 and rec["fanout_results"] >= 1
+    assert rec["fanout_node"] is True  # the node board's first result is the golden, from its owner
 
 
 def test_option_a_r04_binding_deadlocks(tmp_path):
@@ -78,6 +79,7 @@ def test_option_a_flow_on_gpu(tmp_path):
     assert rec["ok"] and rec["mode"] == "gpu"
     assert rec["contexts_opened"] == rec["contexts_closed"] >= 1
     assert rec["cancel_latency_ms"] < 50
+    assert rec["fanout_node"] is True
 
 
 # ---------------------------------------------------------------- C quotes vs INTEGRATION.md Go

@@ -374,15 +374,14 @@ def _never() -> bool:
 
 
 def _native_applies(board: "NodeBoard", world: int) -> bool:
-    """dpow_node_mine decides the node's answer from the board's votes alone: only when the board
-    is shared by exactly `world` ranks, or when one rank runs without a process group.  A local
-    board under a group of world > 1 (or a shared board of another size) would let every rank
-    vote alone and return its own partition's first hit: that case takes the Python loop, whose
-    boundary is the group's all-reduce."""
-    if board.shared:
-        return board.world == world
-    if world != 1:
-        return False
+    """dpow_node_mine decides the node's answer from the board's votes alone: when the board is
+    shared by exactly `world` ranks, or when no process group runs (then the rank's values alone
+    decide, as node_mine's local_only path: one rank, or the one-GPU emulation of
+    tools/node_probe.py).  A local board, or a shared board of another size, under an initialised
+    group would let every rank vote alone and return its own partition's first hit: that case
+    takes the Python loop, whose boundary is the group's all-reduce."""
+    if board.shared and board.world == world:
+        return True
     import torch.distributed as dist
     return not (dist.is_available() and dist.is_initialized())
 

@@ -483,9 +483,9 @@ def test_board_without_attach_keeps_expected_time_batches():
 
 def test_native_loop_only_where_the_board_decides(monkeypatch):
     """node_mine takes dpow_node_mine only when the board's votes decide the node (a
-    board shared by exactly `world` ranks, or one rank without a process group) and no Python
-    `cancelled` predicate is given; a local board under a process group of world > 1 takes the
-    Python loop, whose boundary is the group's all-reduce."""
+    board shared by exactly `world` ranks, or no process group at all) and no Python `cancelled`
+    predicate is given; a local board under a process group takes the Python loop, whose
+    boundary is the group's all-reduce."""
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -523,4 +523,6 @@ def test_native_loop_only_where_the_board_decides(monkeypatch):
         dist.all_reduce = orig
         dist.destroy_process_group()
         board.close()
-    assert N._native_applies(N.NodeBoard.local(), 1) is True  # one rank, no group
+    # no process group: the rank's own values decide (one rank, or the one-GPU emulation)
+    assert N._native_applies(N.NodeBoard.local(), 1) is True
+    assert N._native_applies(N.NodeBoard.local(), 4) is True

@@ -18,6 +18,7 @@
 // entries.  Join and leave take the header's spin lock (a few hundred nanoseconds, once per
 // task and rank); the search itself never does.
 #include <errno.h>
+#include <stdlib.h>
 #include <fcntl.h>
 #include <sched.h>
 #include <string.h>
@@ -25,6 +26,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <time.h>
+
+#include <chrono>
 #include <new>
 #include <string>
 
@@ -49,8 +53,9 @@ struct alignas(64) Header {
     uint64_t magic;
     uint32_t lock;
     uint32_t pad0;
-    uint64_t joins;  // tasks joined over the board's life (diagnostics)
-    uint64_t pad[5];
+    uint64_t tasks;   // task entries created over the board's life (diagnostics)
+    uint64_t shared;  // of which every rank ran on one GPU (one search for the node: dpow_board_search)
+    uint64_t pad[4];
 };
 
 struct alignas(64) Entry {
@@ -60,6 +65,7 @@ struct alignas(64) Entry {
     uint64_t joined;     // bit r: rank r has joined this task
     uint64_t nonce_len;
     uint64_t pad[4];
+    uint64_t dev_key[kMaxWorld];  // rank r's GPU (dpow::device_key; 0: unknown), written before its joined bit
     uint8_t nonce[DPOW_MAX_NONCE];
     dpow_node_slot slot;
     dpow_node_vote_entry votes[2 * kMaxWorld];
@@ -103,6 +109,14 @@ struct dpow_board {
     int fd = -1;
     bool shared = false;
 };
+
+namespace {
+
+int board_join(dpow_board *b, const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t world, uint32_t rank,
+               uint64_t dev_key, Entry **out);
+int same_gpu(const Entry &e, uint32_t world, uint64_t mine, const volatile uint32_t *cancel);
+
+}  // namespace
 
 extern "C" {
 
@@ -171,43 +185,12 @@ int dpow_board_unlink(const char *name) {
 
 int dpow_board_join(dpow_board *b, const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t world,
                     uint32_t rank, dpow_node_slot **slot, dpow_node_vote_entry **votes) {
-    if (!b || !b->mem || !slot || !votes || (nonce_len && !nonce))
-        return dpow::fail(DPOW_EINVAL, "dpow_board_join: NULL argument");
-    if (nonce_len > DPOW_MAX_NONCE) return dpow::fail(DPOW_EINVAL, "dpow_board_join: nonce too long");
-    if (world < 2 || world > kMaxWorld || (world & (world - 1)) != 0 || rank >= world)
-        return dpow::fail(DPOW_EINVAL, "dpow_board_join: world must be a power of two in [2, 64], rank < world");
-    Layout &L = *b->mem;
-    const uint64_t bit = 1ull << rank;
-    Lock lk(&L.h.lock);
-    // The task's entry: the active one with this key that rank has not joined yet (an entry the
-    // rank already joined belongs to an earlier task with the same key whose other ranks are
-    // still leaving it).
-    Entry *free_e = nullptr;
-    for (uint32_t i = 0; i < kEntries; ++i) {
-        Entry &e = L.e[i];
-        if (key_matches(e, nonce, nonce_len, ntz, world) && !(e.joined & bit)) {
-            e.joined |= bit;
-            e.refs++;
-            *slot = &e.slot;
-            *votes = e.votes;
-            return 0;
-        }
-        if (e.state == 0 && !free_e) free_e = &e;
-    }
-    if (!free_e) return dpow::fail(DPOW_ENOMEM, "dpow_board_join: every task entry of the board is in use");
-    Entry &e = *free_e;
-    e.ntz = ntz;
-    e.world = world;
-    e.nonce_len = nonce_len;
-    if (nonce_len) memcpy(e.nonce, nonce, nonce_len);
-    dpow_node_slot_reset(&e.slot);
-    memset(e.votes, 0, sizeof e.votes);
-    e.joined = bit;
-    e.refs = 1;
-    L.h.joins++;
-    __atomic_store_n(&e.state, 1u, __ATOMIC_RELEASE);
-    *slot = &e.slot;
-    *votes = e.votes;
+    if (!slot || !votes) return dpow::fail(DPOW_EINVAL, "dpow_board_join: NULL argument");
+    Entry *e = nullptr;
+    const int rc = board_join(b, nonce, nonce_len, ntz, world, rank, 0, &e);
+    if (rc < 0) return rc;
+    *slot = &e->slot;
+    *votes = e->votes;
     return 0;
 }
 
@@ -223,6 +206,14 @@ int dpow_board_leave(dpow_board *b, dpow_node_slot *slot) {
     // The last rank out frees the entry, whether or not every rank joined (a worker that
     // answered from its cache never does; the others left on their kill).
     if (--e.refs == 0) __atomic_store_n(&e.state, 0u, __ATOMIC_RELEASE);
+    return 0;
+}
+
+int dpow_board_counters(dpow_board *b, uint64_t *tasks, uint64_t *shared_gpu) {
+    if (!b || !b->mem || !tasks || !shared_gpu) return dpow::fail(DPOW_EINVAL, "dpow_board_counters: NULL argument");
+    Lock lk(&b->mem->h.lock);
+    *tasks = b->mem->h.tasks;
+    *shared_gpu = __atomic_load_n(&b->mem->h.shared, __ATOMIC_RELAXED);
     return 0;
 }
 
@@ -244,15 +235,34 @@ int dpow_board_search(dpow_board *b, dpow_ctx *ctx, const uint8_t *nonce, size_t
     if (worker_bits < 1 || (1u << worker_bits) > kMaxWorld || worker_byte >= (1u << worker_bits))
         return dpow::fail(DPOW_EINVAL, "dpow_board_search: needs 1 <= worker_bits <= 6 and worker_byte < 2^worker_bits");
     const uint32_t world = 1u << worker_bits;
-    dpow_node_slot *slot = nullptr;
-    dpow_node_vote_entry *votes = nullptr;
-    int rc = dpow_board_join(b, nonce, nonce_len, ntz, world, worker_byte, &slot, &votes);
+    const uint64_t key = dpow::device_key(ctx);
+    Entry *e = nullptr;
+    int rc = board_join(b, nonce, nonce_len, ntz, world, worker_byte, key, &e);
     if (rc < 0) return rc;
-    uint64_t epoch = 0;  // the entry's votes start at zero (dpow_board_join)
+    dpow_node_slot *const slot = &e->slot;
+    // Ranks that share one GPU (more workers than GPUs: the coordinator mirror's W logical workers
+    // on one device) would split the device W ways and progress in the runtime's time slices, so
+    // the node's answer waited for the slowest one's slice (tools/coord_fresh.py: 1.4-1.9x the
+    // first-arrived race).  Then rank 0 searches every partition of each window (worker_bits 0:
+    // the node's first hit directly) and the others only vote; on distinct GPUs each rank searches
+    // its own partition.
+    const int same = same_gpu(*e, world, key, dpow_cancel_flag(ctx));
+    if (same < 0) {
+        if (same == DPOW_CANCELLED) dpow_node_stop(slot);
+        const std::string err = same == DPOW_CANCELLED ? "" : dpow_last_error();
+        (void)dpow_board_leave(b, slot);
+        return same == DPOW_CANCELLED ? DPOW_CANCELLED : dpow::fail(same, err.c_str());
+    }
+    // DPOW_DIAG_BOARD_SPLIT=1: every rank searches its own partition even on a shared GPU (tests
+    // cover the multi-GPU role on one GPU with it; dpow_diag.h)
+    const char *split = getenv("DPOW_DIAG_BOARD_SPLIT");
+    const int role = same && !(split && split[0] == '1') ? (worker_byte == 0 ? 1 : 2) : 0;
+    if (role == 1) __atomic_fetch_add(&b->mem->h.shared, 1ull, __ATOMIC_RELAXED);
+    uint64_t epoch = 0;  // the entry's votes start at zero (board_join)
     uint32_t batches = 0;
     const uint64_t batch_k = kBatchCandidates >> (8 - worker_bits);
-    rc = dpow::node_mine(ctx, slot, votes, worker_byte, world, &epoch, kVoteTimeoutNs, nonce, nonce_len, ntz, 0,
-                         DPOW_K_LIMIT, 0, batch_k, best_global_idx, secret_out, secret_len, &batches, true);
+    rc = dpow::node_mine(ctx, slot, e->votes, worker_byte, world, &epoch, kVoteTimeoutNs, nonce, nonce_len, ntz, 0,
+                         DPOW_K_LIMIT, 0, batch_k, best_global_idx, secret_out, secret_len, &batches, true, role);
     const std::string err = rc < 0 ? dpow_last_error() : "";
     (void)dpow_board_leave(b, slot);
     if (rc < 0) return dpow::fail(rc, err.c_str());
@@ -261,3 +271,77 @@ int dpow_board_search(dpow_board *b, dpow_ctx *ctx, const uint8_t *nonce, size_t
 }
 
 }  // extern "C"
+
+namespace {
+
+int board_join(dpow_board *b, const uint8_t *nonce, size_t nonce_len, uint32_t ntz, uint32_t world, uint32_t rank,
+               uint64_t dev_key, Entry **out) {
+    if (!b || !b->mem || (nonce_len && !nonce)) return dpow::fail(DPOW_EINVAL, "dpow_board_join: NULL argument");
+    if (nonce_len > DPOW_MAX_NONCE) return dpow::fail(DPOW_EINVAL, "dpow_board_join: nonce too long");
+    if (world < 2 || world > kMaxWorld || (world & (world - 1)) != 0 || rank >= world)
+        return dpow::fail(DPOW_EINVAL, "dpow_board_join: world must be a power of two in [2, 64], rank < world");
+    Layout &L = *b->mem;
+    const uint64_t bit = 1ull << rank;
+    Lock lk(&L.h.lock);
+    // The task's entry: the active one with this key that rank has not joined yet (an entry the
+    // rank already joined belongs to an earlier task with the same key whose other ranks are
+    // still leaving it).
+    Entry *free_e = nullptr;
+    for (uint32_t i = 0; i < kEntries; ++i) {
+        Entry &e = L.e[i];
+        if (key_matches(e, nonce, nonce_len, ntz, world) && !(e.joined & bit)) {
+            e.dev_key[rank] = dev_key;
+            __atomic_store_n(&e.joined, e.joined | bit, __ATOMIC_RELEASE);
+            e.refs++;
+            *out = &e;
+            return 0;
+        }
+        if (e.state == 0 && !free_e) free_e = &e;
+    }
+    if (!free_e) return dpow::fail(DPOW_ENOMEM, "dpow_board_join: every task entry of the board is in use");
+    Entry &e = *free_e;
+    e.ntz = ntz;
+    e.world = world;
+    e.nonce_len = nonce_len;
+    if (nonce_len) memcpy(e.nonce, nonce, nonce_len);
+    dpow_node_slot_reset(&e.slot);
+    memset(e.votes, 0, sizeof e.votes);
+    memset(e.dev_key, 0, sizeof e.dev_key);
+    e.dev_key[rank] = dev_key;
+    e.refs = 1;
+    L.h.tasks++;
+    __atomic_store_n(&e.joined, bit, __ATOMIC_RELEASE);
+    __atomic_store_n(&e.state, 1u, __ATOMIC_RELEASE);
+    *out = &e;
+    return 0;
+}
+
+// Whether every rank of the task searches on this rank's GPU: 1 yes (all W joined, one device
+// key), 0 no (some rank's GPU differs, or is unknown), DPOW_CANCELLED when the rank's cancel flag
+// rises first (its task was killed; a rank that answers from its cache never joins), DPOW_EPROTO
+// after kVoteTimeoutNs.  Every rank reaches the same verdict: "no" is final as soon as one other
+// GPU is seen, "yes" needs the full set of W keys, which all ranks then read alike.
+int same_gpu(const Entry &e, uint32_t world, uint64_t mine, const volatile uint32_t *cancel) {
+    const uint64_t full = world == 64 ? ~0ull : (1ull << world) - 1;
+    const int64_t t0 = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now().time_since_epoch()).count();
+    for (uint64_t it = 0;; ++it) {
+        const uint64_t m = __atomic_load_n(&e.joined, __ATOMIC_ACQUIRE);
+        for (uint32_t r = 0; r < world; ++r)
+            if ((m >> r & 1) && (e.dev_key[r] == 0 || e.dev_key[r] != mine)) return 0;
+        if (m == full) return 1;
+        if (__atomic_load_n(cancel, __ATOMIC_ACQUIRE) != 0u) return DPOW_CANCELLED;
+        if (it < 4096) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        const int64_t t = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now().time_since_epoch()).count();
+        if (t - t0 > kVoteTimeoutNs)
+            return dpow::fail(DPOW_EPROTO, "dpow_board_search: the task's other ranks never joined the board");
+        const struct timespec d = {0, 2000};
+        nanosleep(&d, nullptr);
+    }
+}
+
+}  // namespace

@@ -19,6 +19,7 @@
 #include <sched.h>
 #include <sys/prctl.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <algorithm>
@@ -252,6 +253,7 @@ struct dpow_ctx {
     DiagLaunch diag_l[kDiagLaunches];
     size_t diag_nl = 0;
     int64_t diag_t0 = 0;
+    uint64_t dev_key = 0;  // the GPU's identity across processes: a hash of its PCI bus id (dpow::device_key)
 };
 
 namespace {
@@ -785,6 +787,16 @@ int dpow_open(int device, dpow_ctx **out) {
         return hip_fail(e, "hipGetDeviceProperties");
     }
     c->cus = (uint32_t)prop.multiProcessorCount;
+    {   // FNV-1a of the PCI bus id: the same GPU gives the same key in every process of the host
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, device) != hipSuccess) {
+            (void)hipGetLastError();
+            snprintf(bus, sizeof bus, "ordinal-%d-pid-%d", device, (int)getpid());  // never matches another process
+        }
+        uint64_t h = 1469598103934665603ull;
+        for (const char *q = bus; *q; ++q) h = (h ^ (uint8_t)*q) * 1099511628211ull;
+        c->dev_key = h | 1ull;
+    }
     if (const char *pw = getenv("DPOW_DIAG_POLL_WB")) c->knobs.poll_wb = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_BPC")) c->knobs.bpc = (uint32_t)std::max(0, atoi(pw));
     if (const char *pw = getenv("DPOW_DIAG_CPW")) c->knobs.cpw = (uint32_t)std::max(0, atoi(pw));
@@ -1027,7 +1039,7 @@ extern "C" int dpow_node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_
                               uint64_t batch_k, uint64_t *best_global_idx, uint8_t secret_out[DPOW_MAX_SECRET],
                               size_t *secret_len, uint32_t *batches) {
     return dpow::node_mine(c, slot, votes, rank, world, epoch, vote_timeout_ns, nonce, nonce_len, ntz, k_begin, k_limit,
-                           first_k, batch_k, best_global_idx, secret_out, secret_len, batches, false);
+                           first_k, batch_k, best_global_idx, secret_out, secret_len, batches, false, 0);
 }
 
 // dpow_node_mine; `abandon_on_cancel` (a board search, dpow_board_search): a rank whose cancel flag
@@ -1038,7 +1050,8 @@ extern "C" int dpow_node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_
 int dpow::node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *votes, uint32_t rank, uint32_t world,
                     uint64_t *epoch, int64_t vote_timeout_ns, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,
                     uint64_t k_begin, uint64_t k_limit, uint64_t first_k, uint64_t batch_k, uint64_t *best_global_idx,
-                    uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len, uint32_t *batches, bool abandon_on_cancel) {
+                    uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len, uint32_t *batches, bool abandon_on_cancel,
+                    int role) {
     if (!c || !slot || !epoch || !best_global_idx || !secret_out || !secret_len || !batches)
         return set_error(DPOW_EINVAL, "dpow_node_mine: NULL argument");
     if (world == 0 || (world & (world - 1)) != 0 || world > 256 || rank >= world)
@@ -1063,7 +1076,11 @@ int dpow::node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *vot
         int rc = DPOW_EXHAUSTED;
         if (err == 0) {
             uint64_t best = DPOW_NO_HIT;
-            rc = dpow_search(c, nonce, nonce_len, ntz, rank, wbits, k, ke, &best, sec, &slen);
+            // role 0: this rank's partition; 1: every partition of the node (the ranks share this
+            // GPU, dpow_board_search); 2: none (the role-1 rank covers this one's window)
+            if (role == 2) rc = DPOW_EXHAUSTED;
+            else rc = dpow_search(c, nonce, nonce_len, ntz, role == 1 ? 0 : rank, role == 1 ? 0 : wbits, k, ke, &best,
+                                  sec, &slen);
             if (rc < 0) {
                 err = rc;
                 dpow_node_stop(slot);
@@ -1120,6 +1137,8 @@ int dpow::node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *vot
 }
 
 int dpow::fail(int code, const char *msg) { return set_error(code, msg); }
+
+uint64_t dpow::device_key(const dpow_ctx *c) { return c ? c->dev_key : 0; }
 
 extern "C" {
 

@@ -212,6 +212,7 @@ def lib():
                                            ctypes.c_uint32, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         "dpow_board_leave": (ctypes.c_int, [vp, vp]),
         "dpow_board_tasks": (ctypes.c_int, [vp]),
+        "dpow_board_counters": (ctypes.c_int, [vp, u64p, u64p]),
         "dpow_board_search": (ctypes.c_int, [vp, vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
                                              ctypes.c_uint32, ctypes.c_uint32, u64p, u8p, szp, u32p]),
         "dpow_secret_from_index": (ctypes.c_int, [ctypes.c_uint64, u8p, szp]),

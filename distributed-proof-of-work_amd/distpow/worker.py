@@ -45,6 +45,12 @@ class Board:
         """Task entries in use (0 once every rank of every task has left)."""
         return check(lib().dpow_board_tasks(self._b), "dpow_board_tasks")
 
+    def counters(self):
+        """(task entries created, of which all ranks shared one GPU) over the board's life."""
+        t, sh = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().dpow_board_counters(self._b, ctypes.byref(t), ctypes.byref(sh)), "dpow_board_counters")
+        return t.value, sh.value
+
     def join(self, nonce, num_trailing_zeros, world, rank):
         """(slot, votes) addresses of the task's entry for this rank (dpow_board_join)."""
         n = bytes(nonce)

@@ -236,6 +236,9 @@ int dpow_board_join(dpow_board *b, const uint8_t *nonce, size_t nonce_len, uint3
 int dpow_board_leave(dpow_board *b, dpow_node_slot *slot);
 /* Task entries in use (0 once every joined rank has left). */
 int dpow_board_tasks(dpow_board *b);
+/* Task entries created over the board's life, and of those the tasks whose W ranks all ran on one
+ * GPU (dpow_board_search then searched the node's windows once, on rank 0, instead of W ways). */
+int dpow_board_counters(dpow_board *b, uint64_t *tasks, uint64_t *shared_gpu);
 /* One worker's search of a task on the board: replaces the miner's loop (worker.go:301-400) when
  * the node's W = 2^worker_bits workers share the board.  Joins the task's entry, runs
  * dpow_node_mine for partition worker_byte (rank = worker_byte, world = 2^worker_bits) from k = 0,
@@ -246,7 +249,11 @@ int dpow_board_tasks(dpow_board *b);
  * task's kill: Found or Cancel; the rank leaves at once, without waiting for the others' votes),
  * or another rank's cancel stopped the task; a negative code when a search failed or another
  * rank's did, or a vote timed out (120 s: a rank that never joined).  DPOW_EINVAL unless
- * 1 <= worker_bits <= 6 and worker_byte < 2^worker_bits. */
+ * 1 <= worker_bits <= 6 and worker_byte < 2^worker_bits.
+ * A rank first waits until the task's other ranks have joined or one of them is seen on another
+ * GPU (microseconds: the Mine fan-out's skew).  When all W ranks share one GPU (more workers than
+ * GPUs), rank 0 searches every partition of each window (worker_bits 0) and the others only
+ * vote: the same answer, without splitting one device W ways. */
 int dpow_board_search(dpow_board *b, dpow_ctx *ctx, const uint8_t *nonce, size_t nonce_len, uint32_t ntz,
                       uint32_t worker_byte, uint32_t worker_bits, uint64_t *best_global_idx,
                       uint8_t secret_out[DPOW_MAX_SECRET], size_t *secret_len, uint32_t *owner);

@@ -145,6 +145,10 @@ int dpow_diag_node_post_at(struct dpow_node_slot *slot, uint64_t global_idx, int
  * (round 6: the registry keeps one alias per device).  DPOW_EINVAL when no slot is attached. */
 int dpow_diag_node_alias(struct dpow_ctx *ctx, void **cached, void **lookup);
 
+/* Environment knob (no entry point): DPOW_DIAG_BOARD_SPLIT=1 makes dpow_board_search run every
+ * rank on its own partition even when all ranks share one GPU -- the multi-GPU role, for tests
+ * on a one-GPU box (tests/test_coordinator.py). */
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,15 @@ def test_ranks_of_one_task_share_an_entry():
         assert b.tasks() == 4
 
 
+def test_counters():
+    with Board() as b:
+        assert b.counters() == (0, 0)
+        s, _ = b.join(N1, 7, 4, 0)
+        b.join(N1, 7, 4, 1)
+        b.join(N1, 8, 4, 0)
+        assert b.counters() == (2, 0)  # two tasks; none searched (dpow_board_search counts shared GPUs)
+
+
 def test_a_rank_that_joined_already_starts_the_next_task():
     """Rank 0 joining the same key again belongs to a later task with that key (its earlier
     entry still holds ranks that have not left): a new entry, not the old one."""

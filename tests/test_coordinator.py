@@ -53,7 +53,23 @@ def check_task_protocol(c, token, secret, g):
     assert c.board.tasks() == 0  # every rank left the task's entry
 
 
-def test_config3_four_workers_cold_then_warm(golden):
+def _split(monkeypatch, split):
+    """split: every rank searches its own partition (the multi-GPU role, DPOW_DIAG_BOARD_SPLIT);
+    else the W workers, all on GPU 0 here, run each task as one search of rank 0."""
+    if split:
+        monkeypatch.setenv("DPOW_DIAG_BOARD_SPLIT", "1")
+    else:
+        monkeypatch.delenv("DPOW_DIAG_BOARD_SPLIT", raising=False)
+
+
+def check_roles(c, split):
+    tasks, shared = c.board.counters()
+    assert tasks >= 1 and shared == (0 if split else tasks), (tasks, shared)
+
+
+@pytest.mark.parametrize("split", [False, True], ids=["one_gpu", "per_rank"])
+def test_config3_four_workers_cold_then_warm(golden, monkeypatch, split):
+    _split(monkeypatch, split)
     want, g = golden_secret(golden, N1, 7)
     assert want == bytes([194, 170, 210, 13])
     with Coordinator(4) as c:
@@ -72,21 +88,27 @@ def test_config3_four_workers_cold_then_warm(golden):
         assert acts[-3:] == ["CoordinatorMine", "CacheHit", "CoordinatorSuccess"]
         # lower N is a cache hit too (cached N >= requested)
         assert c.mine(N1, 5) == want
+        check_roles(c, split)
         print(f"config3 cold {cold * 1e3:.1f} ms warm {warm * 1e3:.3f} ms secret {list(s)}")
 
 
-def test_config4_eight_workers_n8(golden):
+@pytest.mark.parametrize("split", [False, True], ids=["one_gpu", "per_rank"])
+def test_config4_eight_workers_n8(golden, monkeypatch, split):
+    _split(monkeypatch, split)
     with Coordinator(8) as c:
         assert c.worker_bits == 3
         for tok, nonce in ((201, N1), (202, [2, 2, 2, 2])):
             want, g = golden_secret(golden, nonce, 8)
             assert c.mine(nonce, 8, token=tok) == want
             check_task_protocol(c, tok, want, g)
+        check_roles(c, split)
     assert golden_secret(golden, N1, 8)[0] == bytes([10, 189, 80, 242])
     assert golden_secret(golden, [2, 2, 2, 2], 8)[0] == bytes([218, 55, 128, 17])
 
 
-def test_config5_two_concurrent_clients(golden):
+@pytest.mark.parametrize("split", [False, True], ids=["one_gpu", "per_rank"])
+def test_config5_two_concurrent_clients(golden, monkeypatch, split):
+    _split(monkeypatch, split)
     reqs = [(N1, 7), ([5, 6, 7, 8], 5), ([2, 2, 2, 2], 5), ([2, 2, 2, 2], 7)]
     with Coordinator(4) as c:
         out = {}
@@ -106,11 +128,15 @@ def test_config5_two_concurrent_clients(golden):
         assert c.cache_entry([2, 2, 2, 2]) == (7, bytes([218, 55, 128, 17]))
         assert not [t for t in c.trace() if t["action"] == "CoordinatorDroppedResult"]
         assert c.board.tasks() == 0
+        check_roles(c, split)
 
 
-def test_worker_cache_hit_in_node_mode(golden):
+@pytest.mark.parametrize("split", [False, True], ids=["one_gpu", "per_rank"])
+def test_worker_cache_hit_in_node_mode(golden, monkeypatch, split):
     """A worker answering from its cache (worker.go:261-299) never joins the task's entry; the
-    other workers leave it on their kill, and the 2W messages still close."""
+    other workers leave it on their kill (waiting for it to join, or in their votes), and the 2W
+    messages still close."""
+    _split(monkeypatch, split)
     want, _ = golden_secret(golden, N1, 6)
     with Coordinator(4) as c:
         # seed worker 2's cache only, as if it alone had served the nonce before; its Found ACK

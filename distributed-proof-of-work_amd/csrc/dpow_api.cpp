@@ -1357,7 +1357,7 @@ int dpow_plan_candidate(const uint8_t *nonce, size_t nonce_len, uint32_t worker_
     // The launch a search from the start of k's chunk-length segment would use
     // (it spans the 2^24-k segments up to k: the segment-word path of the kernel).
     const uint32_t clen = chunk_len_of(k);
-    uint64_t k_first = (!DPOW_SPAN || clen == 0) ? k : 1ull << (8 * (clen - 1));
+    uint64_t k_first = clen == 0 ? k : 1ull << (8 * (clen - 1));
     if (const uint64_t w2 = word2_period((uint32_t)(nonce_len % 64) % 4))  // the planner's W0 + 2 split
         if (k_first < k / w2 * w2) k_first = k / w2 * w2;
     std::vector<PlannedLaunch> plan;

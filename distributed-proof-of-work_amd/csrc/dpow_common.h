@@ -47,19 +47,12 @@ constexpr uint32_t kBop3G = 0xE4;  // G = z ? x : y
 constexpr uint32_t kBop3H = 0x96;  // H = x ^ y ^ z
 constexpr uint32_t kBop3I = 0x39;  // I = y ^ (x | ~z)
 
-// Launches span 2^24-k segments (plan.cpp; the kernel re-derives the constants
-// of the words holding k >> 24).  A/B switch: 0 = the host splits a window at
-// every multiple of 2^24 k, as in round 1.
-#ifndef DPOW_SPAN
-#define DPOW_SPAN 1
-#endif
+// Launches span 2^24-k segments (plan.cpp; the kernel re-derives the constants of the
+// words holding k >> 24); round 1 split a window at every multiple of 2^24 k instead.
 
 // Launches span chunk lengths 1..3 for SH = 0 layouts (plan.cpp lspan_end; the kernel
-// re-derives the pad and bit-length words per chunk length).  A/B switch: 0 = one launch
-// per chunk length, as in round 2.
-#ifndef DPOW_LSPAN
-#define DPOW_LSPAN 1
-#endif
+// re-derives the pad and bit-length words per chunk length); round 2 ran one launch per
+// chunk length.
 
 // Candidates per lane per wave-block (interleaved for ILP).
 #ifndef DPOW_NC
@@ -81,28 +74,22 @@ constexpr uint32_t kClaimSlot = kClaimCounters * kClaimStride;  // one launch's 
 // previous search's launches (Launch::ctrl_next), or at dpow_open -- so a search needs
 // no reset kernel in front of its first launch.
 constexpr unsigned long long kNoHit = 0x7FFFFFFFFFFFFFFFull;  // = DPOW_NO_HIT (include/dpow.h)
-#ifndef DPOW_CTRL_SPLIT
-#define DPOW_CTRL_SPLIT 1  // Ctrl::done on a 128-byte line of its own (A/B switch)
-#endif
 struct Ctrl {
     unsigned long long best;  // min global index found (kNoHit = none), atomicMin target
     uint32_t stop;            // set by the watcher when the host cancel flag is raised
-#if DPOW_CTRL_SPLIT
-    // Every wave loads best and stop once per poll group: the retirement count's atomics
-    // (one per workgroup, at the end of a launch) queue behind those loads on a shared line.
+    // Ctrl::done on a 128-byte line of its own: every wave loads best and stop once per poll
+    // group, and the retirement count's atomics (one per workgroup, at the end of a launch)
+    // queued behind those loads on a shared line.
     uint32_t pad0_;
     unsigned long long pad1_[14];
-#endif
     uint32_t done;            // worker workgroups retired (cumulative within one search)
-#if DPOW_CTRL_SPLIT
     uint32_t pad2_[31];
-#endif
 };
-constexpr uint32_t kCtrlLine = DPOW_CTRL_SPLIT ? 256 : 128;  // bytes per ring entry
+constexpr uint32_t kCtrlLine = 256;  // bytes per ring entry
 constexpr uint32_t kCtrlRing = 4;
 constexpr uint32_t kCtrlStride = kCtrlLine / sizeof(Ctrl);  // Ctrl units between ring entries
 static_assert((kCtrlRing & (kCtrlRing - 1)) == 0 && kCtrlLine % sizeof(Ctrl) == 0, "the ring is aligned to its size");
-static_assert(!DPOW_CTRL_SPLIT || (sizeof(Ctrl) == 256 && __builtin_offsetof(Ctrl, done) == 128), "done on its own line");
+static_assert(sizeof(Ctrl) == 256 && __builtin_offsetof(Ctrl, done) == 128, "done on its own line");
 
 // Host-visible completion record of one launch (pinned, host-coherent, mapped).
 // The launch's last retiring workgroup writes it: the
@@ -141,12 +128,12 @@ struct Launch {
     uint32_t chunk_tail;   // wave-blocks per claim after them (the launch's tail: small claims)
     uint64_t n_big;        // claims of `chunk` wave-blocks
     uint64_t n_chunks;     // claims covering n_wblocks (n_big + tail claims)
-    uint64_t n_head;       // the claims every wave takes at its start (2 per wave): hashed at raised priority
+    uint64_t n_head;       // the claims every wave takes at its start (2 per wave; host diagnostics)
     uint64_t n_static;     // claims [0, n_static) are handed out by wave index, not by a counter: worker
                            //  wave w's first claim is w (the "_ls" kernels only; 0 for every other launch)
     uint32_t poll_wb;      // wave-blocks per group: a wave reads Ctrl::best / Ctrl::stop once per group
-    uint32_t fair_ticks;   // fair priority (one-block kernels, DPOW_FAIR_PRIO): s_memrealtime ticks per wave-block
-                           //  at a fair share of the device, x 1.25; a wave behind that hashes at priority 2
+    uint32_t reserved0;    // (round 4's fair-priority tick count; kept so the kernel argument layout,
+                           //  and with it the kernels' code, stays as measured)
     unsigned long long *claim;  // this launch's kClaimCounters counters (zero at launch start;
                                 //  the launch's last workgroup re-zeroes them for the slot's next user)
     Ctrl *ctrl;              // this search's control block (clean at its first launch)
@@ -256,7 +243,7 @@ DPOW_HD uint32_t wave_uniform_v(uint64_t i0, uint32_t rbits, uint32_t base_tb) {
     const uint64_t R = 1ull << rbits;
     return base_tb | (uint32_t)(i0 & (R - 1)) | ((uint32_t)((i0 >> rbits) & 0xFFFFFFu) << 8);
 }
-// Segment-word additions (DPOW_SPAN): a launch's template holds k >> 24 =
+// Segment-word additions (launches spanning 2^24-k segments): a launch's template holds k >> 24 =
 // seg_first at byte p + 4 (words W0 + 1 and, for SH = 3, W0 + 2); a candidate
 // in 2^24-k segment `seg` adds (seg - seg_first) << 8 SH to that 64-bit word
 // pair.  The field never overflows its bytes within one chunk length, but the

@@ -55,28 +55,9 @@ namespace DPOW_KNS {
 
 // SGPR budget: <= 80 allocated SGPRs admit 8 four-wave workgroups per CU
 // (8 waves per SIMD, MI355X_MICROARCH.md "Residency").  Literal K constants are
-// rematerialised by SALU moves, which co-issue beside other waves' VALU.
-#ifndef DPOW_FOLD_ZERO
-#define DPOW_FOLD_ZERO 1  // fold always-zero message words to literal K (A/B switch)
-#endif
-#ifndef DPOW_WATCH_SLEEP
-#define DPOW_WATCH_SLEEP 16  // watcher poll interval, s_sleep units of 64 cycles (round 4: 32)
-#endif
-#ifndef DPOW_WATCH_BATCH
-#define DPOW_WATCH_BATCH 1  // the watcher loads a poll's words together (0: round 4's poll; A/B switch)
-#endif
-#ifndef DPOW_XCD_RETIRE
-// Retirement counted per claim counter, then on Ctrl::done (A/B switch; 2: out of line): in the
-// chunk-length-spanning units only -- the launches of short searches, below k = 2^24 -- so
-// that the other units' kernels (the sweep's among them) keep their code.
-#define DPOW_XCD_RETIRE (DPOW_VLS ? 1 : 0)
-#endif
-#ifndef DPOW_HIT_EARLY
-#define DPOW_HIT_EARLY 0  // 1: a wave's hit goes to the early-hit word from the hit path (A/B switch)
-#endif
-#ifndef DPOW_STEAL
-#define DPOW_STEAL 1  // a wave whose counter drained claims from the next counter (A/B switch)
-#endif
+// rematerialised by SALU moves, which co-issue beside other waves' VALU.  The budgets are
+// tuning values (tools/isa_loop.py builds with others); DESIGN.md records the A/B
+// measurements of the alternatives that were removed from this file in round 6.
 #ifndef DPOW_NUM_SGPR
 #define DPOW_NUM_SGPR 72
 #endif
@@ -86,75 +67,28 @@ namespace DPOW_KNS {
 #ifndef DPOW_NUM_SGPR_W15
 #define DPOW_NUM_SGPR_W15 100  // two-block layouts at W0 = 15 (kW15Sgpr below)
 #endif
-#ifndef DPOW_SGPR_LONG_W0
-#define DPOW_SGPR_LONG_W0 8
-#endif
+constexpr int kSgprLongW0 = 8;
+// The watcher's poll interval, s_sleep units of 64 cycles (round 4: 32).
+constexpr int kWatchSleep = 16;
 // A wave polls Ctrl::best / Ctrl::stop once per group of Launch::poll_wb wave-blocks
-// of a chunk (the host's choice: plan.h launch_poll_wb); DPOW_POLL_WB = 0 builds the
-// once-per-chunk loop instead (A/B switch).  profiles/r01_ab_poll.log: 0 / 12 / 16 / 32
+// of a chunk (the host's choice: plan.h launch_poll_wb; DPOW_POLL_WB = 16 for long
+// searches).  profiles/r01_ab_poll.log: once per chunk / 12 / 16 / 32 wave-blocks
 // -> 216.3 / 217.8 / 218.3 / 218.6 GH/s, time-to-secret N=7 1.57 / 1.47 / 1.49 / 1.56 ms.
 #ifndef DPOW_POLL_WB
 #define DPOW_POLL_WB 16
 #endif
-// Tail priority (see the claim loop): profiles/r01_ab_tail_prio.log, sweep windows at
-// workerBits 3 (2^29-candidate launches) 209.5 -> 212.8 GH/s, workerBits 0 217.4 -> 218.3.
-#ifndef DPOW_TAIL_PRIO
-#define DPOW_TAIL_PRIO 1
-#endif
-#ifndef DPOW_HEAD_PRIO
-#define DPOW_HEAD_PRIO 0  // A/B switch (needs DPOW_TAIL_PRIO)
-#endif
-// A wave requests its next claim while it hashes the current chunk (1), or only
-// once that chunk is done (0: one claim in flight per wave, so a first hit
-// waits for fewer chunks below it; A/B switch).  profiles/r02_ab_ahead.log:
-// 1 / 0 -> 217.6 / 215.5 GH/s, time-to-secret N = 7 1.35-1.40 / 1.33-1.34 ms, N = 8
-// 19.1 / 19.3 ms: the claim's latency shows, the shorter drain does not.
-#ifndef DPOW_CLAIM_AHEAD
-#define DPOW_CLAIM_AHEAD 1
-#endif
+// Retirement counted per claim counter, then on Ctrl::done: in the chunk-length-spanning
+// units only -- the launches of short searches, below k = 2^24 -- so that the other units'
+// kernels (the sweep's among them) keep their code.
+constexpr bool kXcdRetire = DPOW_VLS != 0;
 // Static first claims (the "_ls" kernels: the short launches below k = 2^24 that the
 // time-to-secret path runs): worker wave w's first claim is chunk w, so a wave starts
 // hashing without waiting for a contended counter -- at 4 workgroups per CU the start-up
 // burst of 8k claim atomics on 8 counters held the median wave 5 us and the slowest 10 us
 // before its first wave-block (tools/wave_trace_tts.py).  Its claim-ahead atomic then
 // hides behind that first chunk.  The counters hand out chunks from Launch::n_static on.
-#ifndef DPOW_STATIC_FIRST
-#define DPOW_STATIC_FIRST DPOW_VLS
-#endif
-// The claim-ahead atomic in the chunk's last poll group instead of its first (one-block
-// kernels): a wave then reserves its next chunk only near the end of the current one, so a
-// slow wave does not sit on an early chunk for the whole of its current one, and the polls of
-// the chunk's earlier groups do not wait for the claim atomic (vmcnt counts in issue order).
-// Round 4, five same-box A/Bs of the sweep (tools/ab_variants.py, profiles/r04_node_ab.log):
-// +0.03 to +0.24 % (218.15-218.95 against 217.91-218.48 GH/s); an 8-GPU rank's
-// [2,2,2,2]/8 0.358-0.374 against 0.376-0.378 ms, the other node cases within noise.
-#ifndef DPOW_CLAIM_LATE
-#define DPOW_CLAIM_LATE 1
-#endif
-// A fresh read of Ctrl::best / Ctrl::stop at the end of each chunk (one-block kernels), for
-// the check at the next claim: the group's poll was issued at the group's start, so a wave
-// whose chunk ended after a hit elsewhere would start one more chunk above it and hash a
-// whole group of it (tools/wave_trace_node.py: the last waves of an 8-GPU rank's
-// [1,2,3,4]/7 search exited 8-28 us after the hit, on chunks above it).  Issued before the
-// claim is taken, consumed at the check: its latency overlaps the claim's.
-#ifndef DPOW_CLAIM_FRESH
-#define DPOW_CLAIM_FRESH 0
-#endif
-// Fair priority (one-block kernels): the SIMD's arbiter issues its oldest wave first, so the
-// youngest waves of a grid progress at a fraction of the others' rate, and the chunks they
-// hold delay a first hit and the drain behind it.  With it a wave compares the wave-blocks it
-// has hashed with what a fair share of the device would have hashed since it started
-// (Launch::fair_ticks per wave-block, from s_memrealtime) at each poll group, and hashes at
-// priority 2 while it is behind.  (A first version compared the chunk with its counter's
-// frontier, read with every poll group; those loads of the claim counters' lines slowed the
-// claims and an 8-GPU rank's N = 8 search 2.5x.)
-#ifndef DPOW_FAIR_PRIO
-#define DPOW_FAIR_PRIO 0
-#endif
-#ifndef DPOW_CLAIM_DEFER
-#define DPOW_CLAIM_DEFER 1  // read the claim-ahead's result after the chunk, not before it (A/B switch;
-                            // one final block only, search_body kDeferClaims)
-#endif
+// (plan.cpp sets Launch::n_static for exactly those launches.)
+constexpr bool kStaticFirst = DPOW_VLS != 0;
 // Diagnostic builds only (tools/wave_trace.py, tools/wave_trace_node.py): every worker wave
 // records kTraceFields words -- {start, first claim, exit} in s_memrealtime ticks (100 MHz),
 // its hashed wave-blocks, the start of its last chunk and that chunk's claim index, why it
@@ -185,15 +119,6 @@ DPOW_DEV uint32_t md5_fn(uint32_t x, uint32_t y, uint32_t z) {
 // an opaque v_mov (so they are not folded back to SGPRs), they cost nothing in
 // the loop: v_add3_u32 reads a VGPR operand at the same rate.  Capped so the
 // kernel stays within 64 VGPRs (8 waves/SIMD).
-#ifndef DPOW_VGPR_K
-#define DPOW_VGPR_K 1  // A/B switch
-#endif
-#ifndef DPOW_VGPR_K_MAX
-#define DPOW_VGPR_K_MAX -1  // >= 0: one cap for every layout (A/B); -1: VgprK::kCap
-#endif
-#ifndef DPOW_VGPR_K_MIN
-#define DPOW_VGPR_K_MIN 0  // layouts with fewer eligible constants keep them all in SGPRs
-#endif
 
 struct KConst {
     uint32_t v[128];  // [64 * BLK + I]; only the entries VgprK selects are set
@@ -205,9 +130,7 @@ struct KConst {
 // (plan.cpp), so their K + M constants are re-derived per wave when it enters
 // another segment: word W0 + 1 always, W0 + 2 when SH = 3 (the two-byte field
 // of L = 5 crosses into it).
-#if DPOW_SPAN && DPOW_POLL_WB == 0
-#error "DPOW_SPAN needs the grouped chunk loop (DPOW_POLL_WB > 0)"
-#endif
+static_assert(DPOW_POLL_WB > 0, "the chunk loop polls per group of wave-blocks");
 // For SH != 0 word W0 + 1 also holds the top bytes of V; its K + M is then
 // wave-uniform per wave-block anyway (VarWords::hi_s, which carries the
 // segment addition too), so only SH = 0's W0 + 1 and SH = 3's W0 + 2 are
@@ -216,7 +139,7 @@ struct KConst {
 // there the bit-length word (16 NBLK - 2) and W0 + 1 (the pad of L = 3) change per segment.
 template <int NBLK, int W0, int SH>
 DPOW_DEV_CONST bool seg_word(int m) {
-    return (DPOW_SPAN && ((SH == 0 && m == W0 + 1) || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2))) ||
+    return (SH == 0 && m == W0 + 1) || (SH == 3 && m == W0 + 2 && m != 16 * NBLK - 2) ||
            (DPOW_VLS && SH == 0 && (m == W0 + 1 || m == 16 * NBLK - 2));
 }
 
@@ -225,14 +148,9 @@ DPOW_DEV_CONST bool seg_word(int m) {
 // the steps (some state words are wave-uniform there, and it exploits that).
 // Which start issues best depends on the layout; the table is the argmax of a
 // per-layout sweep of builds with one start for every layout
-// (DPOW_PIPE_LEAD = 1..6, tools/lead_sweep.py, profiles/r02_lead_sweep.json),
+// (one start for every layout, 1..6: tools/lead_sweep.py, profiles/r02_lead_sweep.json),
 // where a start beats 4 by >= 0.8 %.  The headline <1,1,0> keeps 4.
-// DPOW_PIPE_LEAD > 0 forces one start for every layout (A/B builds).
-#ifndef DPOW_PIPE_LEAD
-#define DPOW_PIPE_LEAD 0
-#endif
 constexpr int pipe_lead(int nblk, int w0, int sh) {
-    if (DPOW_PIPE_LEAD > 0) return DPOW_PIPE_LEAD;
     // (round 4: the same sweep over the round-4 kernels, profiles/r04_lead_sweep.json, moved the
     // entries marked r4 -- a start that beats the table's by >= 1 % -- and dropped <1,10,1..2>'s
     // 3, now 7.4 % below 4)
@@ -285,7 +203,7 @@ struct VgprK {
     static constexpr bool seg(int blk, int i) { return seg_word<NBLK, W0, SH>(16 * blk + md5_word(i)) && run(blk, i); }
     static constexpr bool eligible(int blk, int i) {
         const int m = 16 * blk + md5_word(i);
-        const bool zero = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
+        const bool zero = m > W0 + 2 && m != 16 * NBLK - 2;
         const bool lane = m == W0 || (SH != 0 && m == W0 + 1);
         const bool piped = blk > 0 || i >= kI0;
         return !zero && !lane && piped && run(blk, i) && !seg(blk, i);
@@ -317,13 +235,11 @@ struct VgprK {
     // (round 4, profiles/r04_lead_sweep.json: a cap of 24 for <1,7,1..2> +1.9-2.0 %,
     // <1,4,3> +1.5 %, <1,5,3> +1.0 %; elsewhere it is no better, or costs up to 3 %)
     static constexpr bool kCap24 = NBLK == 1 && ((W0 == 7 && (SH == 1 || SH == 2)) || (SH == 3 && (W0 == 4 || W0 == 5)));
-    static constexpr int kCap = DPOW_VGPR_K_MAX >= 0 ? DPOW_VGPR_K_MAX
-                                : kCap24 ? 24
+    static constexpr int kCap = kCap24 ? 24
                                 : NBLK == 1 ? (SH == 0 ? 24 : SH == 3 ? 14 : 18)
                                             : (SH == 3 ? 20 : 26);
     static constexpr bool use(int blk, int i) {
-        return seg(blk, i) || (DPOW_VGPR_K && count() >= DPOW_VGPR_K_MIN && eligible(blk, i) &&
-                               rank(blk, i) < kCap - count_seg());
+        return seg(blk, i) || (eligible(blk, i) && rank(blk, i) < kCap - count_seg());
     }
 };
 
@@ -409,7 +325,7 @@ struct StepWord {
     // Words past the variable bytes, the chunk tail and the 0x80 pad -- every
     // word after W0 + 2 except the bit-length word -- are zero for every launch
     // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
-    static constexpr bool zero_word = DPOW_FOLD_ZERO && m > W0 + 2 && m != 16 * NBLK - 2;
+    static constexpr bool zero_word = m > W0 + 2 && m != 16 * NBLK - 2;
     static constexpr bool per_lane = m == W0 || (SH == 3 && m == W0 + 1);  // K + M differs per lane
     static constexpr bool vgpr_k = VgprK<NBLK, W0, SH>::use(BLK, I);
     static constexpr bool seg = seg_word<NBLK, W0, SH>(m);
@@ -446,7 +362,7 @@ DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &
 // instructions, two full rate (v_bitop3_b32, v_add_u32) and two half rate
 // (v_add3_u32, v_alignbit_b32), strictly dependent within a candidate.
 // Candidate q runs half a step behind candidate p and the two chains alternate
-// instruction by instruction (DPOW_PIPE_ORDER below), with s_nop padding after
+// instruction by instruction (DPOW_PIPE_BODY below), with s_nop padding after
 // the half-rate instructions.  One asm statement per step pair: the compiler
 // keeps the order, allocates the registers and places the SALU moves of the K
 // constants, and adds no padding of its own inside the group (these plain VALU
@@ -476,79 +392,32 @@ template <int I> struct Roles {
 // padding after the full-rate ops 168-185; no rotate padding 179-180.  Order 2
 // (profiles/r01_ab_order.log): the same s_nop 0 / s_nop 2 is best, 214.7; no
 // padding 170.7; add3 padding 1 or 3: 210.
-#ifndef DPOW_NOP_B
-#define DPOW_NOP_B -1  // after v_bitop3_b32
-#endif
-#ifndef DPOW_NOP_R
-#define DPOW_NOP_R 0  // after v_alignbit_b32 (the rotate; the next add reads it)
-#endif
-#ifndef DPOW_NOP_D
-#define DPOW_NOP_D -1  // after v_add_u32
-#endif
-#ifndef DPOW_NOP_A
-#define DPOW_NOP_A 2  // after v_add3_u32
-#endif
-#define DPOW_STR2(x) #x
-#define DPOW_STR(x) DPOW_STR2(x)
-#if DPOW_NOP_B >= 0
-#define DPOW_PAD_B "s_nop " DPOW_STR(DPOW_NOP_B) "\n\t"
-#else
-#define DPOW_PAD_B ""
-#endif
-#if DPOW_NOP_R >= 0
-#define DPOW_PAD_R "s_nop " DPOW_STR(DPOW_NOP_R) "\n\t"
-#else
-#define DPOW_PAD_R ""
-#endif
-#if DPOW_NOP_D >= 0
-#define DPOW_PAD_D "s_nop " DPOW_STR(DPOW_NOP_D) "\n\t"
-#else
-#define DPOW_PAD_D ""
-#endif
-#if DPOW_NOP_A >= 0
-#define DPOW_PAD_A "s_nop " DPOW_STR(DPOW_NOP_A) "\n\t"
-#else
-#define DPOW_PAD_A ""
-#endif
+#define DPOW_PAD_R "s_nop 0\n\t"  // after v_alignbit_b32 (the rotate; the next add reads it)
+#define DPOW_PAD_A "s_nop 2\n\t"  // after v_add3_u32
 
 // Order of a step pair (B bop3, A add3, R rotate, D add; p at step I, q finishing
-// step I-1 then starting step I).  2 (default): p.B q.R p.A q.D p.R q.B p.D q.A --
-// the two chains strictly alternate, so every dependency is two instructions
-// apart (F H H F H F F H); 214.7 GH/s.  1: p.B q.R q.D p.A q.B p.R p.D q.A --
-// F and H strictly alternate, but each rotate sits right before its add;
-// 209.1 GH/s.  (Two pairs interleaved at NC = 4 with both properties, every
-// dependency >= 3 apart: 191 GH/s at best.  profiles/r01_ab_order.log.)
-#ifndef DPOW_PIPE_ORDER
-#define DPOW_PIPE_ORDER 2
-#endif
-#if DPOW_PIPE_ORDER == 1
-#define DPOW_PIPE_BODY                                                     \
-    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \
-    "v_alignbit_b32 %[rq], %[tq], %[tq], %[sq]\n\t" DPOW_PAD_R            \
-    "v_add_u32_e32 %[qb], %[qc], %[rq]\n\t" DPOW_PAD_D                    \
-    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A                \
-    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" DPOW_PAD_B \
-    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R            \
-    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t" DPOW_PAD_D                    \
+// step I-1 then starting step I): p.B q.R p.A q.D p.R q.B p.D q.A -- the two chains
+// strictly alternate, so every dependency is two instructions apart (F H H F H F F H);
+// 214.7 GH/s.  (p.B q.R q.D p.A q.B p.R p.D q.A -- F and H strictly alternate, but each
+// rotate sits right before its add -- 209.1 GH/s; two pairs interleaved at NC = 4 with
+// both properties, every dependency >= 3 apart: 191 GH/s at best.
+// profiles/r01_ab_order.log.)
+#define DPOW_PIPE_BODY                                        \
+    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" \
+    "v_alignbit_b32 %[rq], %[tq], %[tq], %[sq]\n\t" DPOW_PAD_R \
+    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A     \
+    "v_add_u32_e32 %[qb], %[qc], %[rq]\n\t"                   \
+    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R \
+    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" \
+    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t"                   \
     "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
-#else
-#define DPOW_PIPE_BODY                                                     \
-    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \
-    "v_alignbit_b32 %[rq], %[tq], %[tq], %[sq]\n\t" DPOW_PAD_R            \
-    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A                \
-    "v_add_u32_e32 %[qb], %[qc], %[rq]\n\t" DPOW_PAD_D                    \
-    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R            \
-    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" DPOW_PAD_B \
-    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t" DPOW_PAD_D                    \
-    "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
-#endif
 
-#define DPOW_PIPE_PRO                                                      \
-    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" DPOW_PAD_B \
-    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A                \
-    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" DPOW_PAD_B \
-    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R            \
-    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t" DPOW_PAD_D                    \
+#define DPOW_PIPE_PRO                                         \
+    "v_bitop3_b32 %[fp], %[pb], %[pc], %[pd] bitop3:%[tt]\n\t" \
+    "v_add3_u32 %[tp], %[pa], %[fp], %[kp]\n\t" DPOW_PAD_A     \
+    "v_bitop3_b32 %[fq], %[qb], %[qc], %[qd] bitop3:%[tt]\n\t" \
+    "v_alignbit_b32 %[tp], %[tp], %[tp], %[sp]\n\t" DPOW_PAD_R \
+    "v_add_u32_e32 %[pa], %[pb], %[tp]\n\t"                   \
     "v_add3_u32 %[tq], %[qa], %[fq], %[kq]\n\t" DPOW_PAD_A
 
 // One step pair of candidates p = J, q = J + 1 at step I (q finishes step I-1,
@@ -632,16 +501,10 @@ DPOW_DEV void steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
 
 #undef DPOW_PIPE_BODY
 #undef DPOW_PIPE_PRO
-#undef DPOW_PAD_B
 #undef DPOW_PAD_R
-#undef DPOW_PAD_D
 #undef DPOW_PAD_A
 
 }  // namespace pipe
-
-#ifndef DPOW_PIPE
-#define DPOW_PIPE 1  // hand-ordered alternating issue for the two-candidate hash (A/B switch)
-#endif
 
 // Final-block compression(s) of NCAND candidates; returns the digest words.
 // With ONLY_D the last block stops after step 61, which writes D (steps 62-63
@@ -659,7 +522,7 @@ DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords 
     // The hand-ordered pipeline starts at step W0 + pipe_lead of the first block
     // (all four state words are per-lane from W0 + 4 on; earlier steps are
     // wave-uniform or partly so, and the compiler folds them).
-    constexpr bool kPipe = DPOW_PIPE && NCAND == kNC && (kNC == 2 || kNC == 4);
+    constexpr bool kPipe = NCAND == kNC && (kNC == 2 || kNC == 4);
     constexpr int kEnd0 = (ONLY_D && NBLK == 1) ? 62 : 64;
     constexpr int kLead = pipe_lead(NBLK, W0, SH);
     constexpr int kI0 = kPipe ? (W0 + kLead < kEnd0 ? W0 + kLead : kEnd0) : kEnd0;
@@ -766,30 +629,6 @@ __device__ __attribute__((noinline)) void publish(Ctrl *ctrl, Snap *snap, uint32
 #endif
 }
 
-#if DPOW_XCD_RETIRE == 2
-// The retirement of one worker workgroup (its thread 0), out of line so that its code does not
-// enter the hash kernels' register allocation: counted per claim counter first (worker block b
-// serves counter (b - 1) % 8, its XCD's) on a word of that counter's line, and the counter's
-// last workgroup adds the counter's count to Ctrl::done -- a launch's few hundred to ~1500
-// retirements no longer queue on one line (~100 atomics per us) at its end.  The workgroup
-// that completes Ctrl::done publishes the record.
-__device__ __attribute__((noinline)) void retire(Ctrl *ctrl, Snap *snap, uint32_t seq, unsigned long long *claim,
-                                                 Ctrl *ctrl_next, uint32_t done_target) {
-    const uint32_t n_wg = gridDim.x - 1u;
-    const uint32_t xr = (blockIdx.x - 1u) % kClaimCounters;
-    const uint32_t nx = n_wg / kClaimCounters + (xr < n_wg % kClaimCounters ? 1u : 0u);
-    unsigned long long *const xc = claim + xr * kClaimStride + 2;
-    const unsigned long long px = __hip_atomic_fetch_add(xc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (px + 1ull != (unsigned long long)nx) return;
-    __hip_atomic_store(xc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the slot's next launch
-    const uint32_t prev = __hip_atomic_fetch_add(&ctrl->done, nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if DPOW_WAVE_TRACE
-    if (prev + nx == done_target) g_wave_trace[kTraceFields * (kTraceWaves - 2) + 2] = __builtin_amdgcn_s_memrealtime();
-#endif
-    if (prev + nx == done_target) publish(ctrl, snap, seq, claim, ctrl_next);
-}
-#endif
-
 // Workgroup 0, one lane: relays the host cancel flag to Ctrl::stop while the
 // launch runs; exits once every worker workgroup has retired.  A launch that
 // was still queued when its search returned CANCELLED stops too, even after
@@ -816,33 +655,10 @@ __device__ __attribute__((noinline)) void retire(Ctrl *ctrl, Snap *snap, uint32_
 // watcher workgroup is dispatched first, and the kernel time in the completion record
 // replaces per-launch HIP timing events, whose profiling packets cost the host ~4.5 us per
 // launch on the time-to-secret path (tools/small_search_probe.py, DPOW_DIAG_NO_EVENTS).
-#ifndef DPOW_WATCH_PAD
-#define DPOW_WATCH_PAD 0
-#endif
-#ifndef DPOW_PROLOGUE_PAD
-#define DPOW_PROLOGUE_PAD 0
-#endif
-#ifdef DPOW_VLS
-#define DPOW_VLS_UNIT DPOW_VLS
-#else
-#define DPOW_VLS_UNIT 0
-#endif
-#ifndef DPOW_PAD_4B
-#define DPOW_PAD_4B (DPOW_WATCH_BATCH ? 63 : 0)  // see search_body
-#endif
-#ifndef DPOW_WATCH_NOINLINE
-#define DPOW_WATCH_NOINLINE 0
-#endif
-#if DPOW_WATCH_NOINLINE
-__device__ __attribute__((noinline)) void watcher(const Launch &L) {
-#else
+// The code-placement pad of the sweep kernels (search_body): 63 s_nop.
+constexpr int kPad4B = 63;
 DPOW_DEV void watcher(const Launch &L) {
-#endif
     if (threadIdx.x != 0) return;
-#if DPOW_WATCH_PAD > 0
-    // Code-placement padding (A/B: the hash loop's start alignment follows the code before it)
-    asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(DPOW_WATCH_PAD));
-#endif
     __hip_atomic_store(&L.claim[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long node_seen = ~0ull, bound_seen = L.bound0, early_seen = kNoHit;
 #if DPOW_WAVE_TRACE
@@ -852,10 +668,8 @@ DPOW_DEV void watcher(const Launch &L) {
     wt[0] = __builtin_amdgcn_s_memrealtime();
     wt[1] = wt[2] = 0;
 #endif
-#if DPOW_WATCH_BATCH
     // Every word of a poll is loaded at once and waited for together: one round trip to the
-    // host's pinned pages per poll.  Round 4's loop (DPOW_WATCH_BATCH 0, below) consumed each
-    // load before issuing the next -- the completion count, the best, then the flags, the bound
+    // host's pinned pages per poll.  Round 4's loop consumed each load before issuing the next -- the completion count, the best, then the flags, the bound
     // and the node's words: four round trips, ~8 us per poll under load
     // (tools/search_timeline.py, profiles/r05_ab.json[r05s/]), which every relay waited for:
     // an owner's hit to its early-hit word, another rank's posted hit into Ctrl::best, the
@@ -904,53 +718,8 @@ DPOW_DEV void watcher(const Launch &L) {
             __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
+        __builtin_amdgcn_s_sleep(kWatchSleep);
     }
-#else
-    for (;;) {
-        const uint32_t done = __hip_atomic_load(&L.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done >= L.done_target) {
-#if DPOW_WAVE_TRACE
-            wt[3] = __builtin_amdgcn_s_memrealtime();
-#endif
-            return;
-        }
-        if (L.early) {
-            const unsigned long long b = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (b < early_seen) {
-#if DPOW_WAVE_TRACE
-                if (wt[2] == 0) wt[2] = __builtin_amdgcn_s_memrealtime();
-#endif
-                early_seen = b;
-                __hip_atomic_store(L.early, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        const uint32_t stale = __hip_atomic_load(L.stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        bool stop = __hip_atomic_load(L.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
-                    (int32_t)(stale - L.seq) >= 0;
-        const unsigned long long eb = __hip_atomic_load(L.ext_bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (eb < bound_seen) {
-            bound_seen = eb;
-            __hip_atomic_fetch_min(&L.ctrl->best, eb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (L.node_best) {
-            const unsigned long long nb = __hip_atomic_load(L.node_best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (nb < node_seen) {
-#if DPOW_WAVE_TRACE
-                if (wt[1] == 0 && nb < kNoHit) wt[1] = __builtin_amdgcn_s_memrealtime();
-#endif
-                node_seen = nb;
-                __hip_atomic_fetch_min(&L.ctrl->best, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            stop = stop || __hip_atomic_load(L.node_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
-        }
-        if (stop) {
-            __hip_atomic_store(&L.ctrl->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(DPOW_WATCH_SLEEP);
-    }
-#endif
 }
 
 // One returning atomic per claim, by lane 0 (claim_issue); its result stays in
@@ -1051,13 +820,6 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
                     const unsigned long long prev = __hip_atomic_fetch_min(
                         &L.ctrl->best, (unsigned long long)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("; dpow: atomicMin performed (%0)" ::"v"(prev));
-#if DPOW_HIT_EARLY
-                    // With a node slot attached, a hit that lowered Ctrl::best goes to the pinned
-                    // early-hit word at once (the host verifies and posts it to the node), not at
-                    // the watcher's next poll.
-                    if (L.early != nullptr && prev > (unsigned long long)g)
-                        __hip_atomic_store(L.early, (unsigned long long)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
                 }
                 return g;
             }
@@ -1082,7 +844,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
 // (The attribute takes no template-dependent value: three kernel templates share
 // one body, and md5_variant.hip instantiates the one kLongSgpr / kW15Sgpr select.)
 template <int NBLK, int W0>
-constexpr bool kLongSgpr = NBLK == 2 || W0 >= DPOW_SGPR_LONG_W0;
+constexpr bool kLongSgpr = NBLK == 2 || W0 >= kSgprLongW0;
 template <int NBLK, int W0, int SH>
 constexpr bool kW15Sgpr = (NBLK == 2 && W0 == 15) || (NBLK == 2 && SH == 3 && (W0 == 13 || W0 == 14)) ||
                           (NBLK == 1 && W0 == 11 && SH == 3);
@@ -1108,33 +870,24 @@ DPOW_DEV void search_body(const Launch &L) {
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_first = 0, n_wb = 0, t_last = 0, c_last = 0, reason = 0, t_hit = 0;
 #endif
-#if DPOW_PROLOGUE_PAD > 0
-    // Code-placement padding of the worker path (A/B builds: the hash loop's placement follows
-    // the code in front of it).
-    asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(DPOW_PROLOGUE_PAD));
-#endif
-#if DPOW_PAD_4B > 0
     // The 4-byte-nonce D-equality kernel (<1,1,0,eq>, the sweep's and N >= 8's), not the
-    // chunk-length-spanning unit: DPOW_PAD_4B s_nop in front of the worker path put its hash
+    // chunk-length-spanning unit: kPad4B s_nop in front of the worker path put its hash
     // block at round 4's offset modulo 256 (tests/test_isa.py checks it).  Any change to the
     // watcher re-runs the whole kernel's register allocation (it is inlined: a noinline
     // watcher costs the hash block 24 VALU per wave-block), and the one-round-trip poll moved
     // the hash block by 4 bytes; a move of that kind alone cost the sweep 0.5 % in round 5
     // (profiles/r05_ab.json[r05q/ab.log]).  Padded: 218.8 vs 218.7 GH/s ([r05s/ab.log]).
-    if constexpr (EQ && NBLK == 1 && W0 == 1 && SH == 0 && !DPOW_VLS_UNIT)
-        asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(DPOW_PAD_4B));
-#endif
+    if constexpr (EQ && NBLK == 1 && W0 == 1 && SH == 0 && !DPOW_VLS)
+        asm volatile(".rept %0\n s_nop 0\n .endr" ::"i"(kPad4B));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t loff = lane_offset(L.rbits, lane);
     KConst kc;
     kconst_init<NBLK, W0, SH, 0, 0>(kc, L);
-#if DPOW_SPAN
     // The 2^24-k segment kc's segment-word constants belong to; kept in a VGPR
     // (wave-uniform, read once per group): an SGPR live across the hash loop
     // costs spill reloads inside it under the 80-SGPR budget.
     uint32_t cur_seg_v;
     asm("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(L.seg0));
-#endif
     // SH = 0: the lane offset plus the current segment's addition to word W0 (the 0x80 pad
     // of chunk lengths <= 2 in launches spanning chunk lengths; 0 in the template's own
     // segment), the per-lane part of W0's K + M.
@@ -1154,50 +907,41 @@ DPOW_DEV void search_body(const Launch &L) {
     // least min(n_chunks, 8) worker blocks, so every counter holding a chunk
     // has waves.  Workgroups go round-robin to XCDs, so each counter's waves
     // share one XCD.
-#if DPOW_TAIL_PRIO
-    // Older waves win the SIMD's issue arbitration, so the youngest waves of a
-    // CU barely progress until the launch drains, and then finish chunks they
-    // claimed early.  Every worker wave runs at priority 1 and drops to 0 once
-    // it holds a tail claim: the waves still on earlier chunks issue first.
-#if DPOW_HEAD_PRIO
-    __builtin_amdgcn_s_setprio(2);
-#else
+    // Tail priority: older waves win the SIMD's issue arbitration, so the youngest waves of
+    // a CU barely progress until the launch drains, and then finish chunks they claimed
+    // early.  Every worker wave runs at priority 1 and drops to 0 once it holds a tail
+    // claim: the waves still on earlier chunks issue first.  profiles/r01_ab_tail_prio.log:
+    // sweep windows at workerBits 3 (2^29-candidate launches) 209.5 -> 212.8 GH/s,
+    // workerBits 0 217.4 -> 218.3.
     __builtin_amdgcn_s_setprio(1);
-#endif
-#endif
-    // The deferred claim read holds the claim's value in two more VGPRs across the hash
-    // loop; the two-block kernels sit at 71-79 VGPRs, where that costs a wave per SIMD
-    // or shifts their register assignment (-5 to -10 %, profiles/r02_ab_layouts/), so
-    // they keep the claim read in front of the chunk.
-    constexpr bool kDeferClaims = DPOW_CLAIM_DEFER && NBLK == 1;
-    constexpr bool kLate = DPOW_CLAIM_LATE && kDeferClaims && DPOW_POLL_WB > 0;
-    constexpr bool kFresh = DPOW_CLAIM_FRESH && NBLK == 1;
-    constexpr bool kFair = DPOW_FAIR_PRIO && NBLK == 1 && DPOW_POLL_WB > 0 && DPOW_TAIL_PRIO && !DPOW_HEAD_PRIO;
-    // kFair: the wave's start (s_memrealtime) and its wave-blocks, in VGPRs (wave-uniform; an
-    // SGPR live across the hash loop costs spill reloads inside it)
-    uint32_t fair_t0_v = 0, fair_wb_v = 0;
-    if constexpr (kFair) {
-        const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-        asm volatile("v_mov_b32 %0, %1" : "=v"(fair_t0_v) : "s"(t0));
-        asm volatile("v_mov_b32 %0, 0" : "=v"(fair_wb_v));
-    }
+    // A wave requests its next claim while it hashes the current chunk (profiles/
+    // r02_ab_ahead.log: 217.6 against 215.5 GH/s for one claim in flight per wave).  With
+    // kDeferClaims (one-block kernels) the claim's atomic is issued in the chunk's last poll
+    // group and its result read after the chunk: a slow wave does not sit on an early chunk
+    // for the whole of its current one, and the polls of the chunk's earlier groups do not
+    // wait for the claim atomic (vmcnt counts in issue order; round 4, profiles/
+    // r04_node_ab.log: +0.03 to +0.24 %).  The deferred read holds the claim's value in two
+    // more VGPRs across the hash loop; the two-block kernels sit at 71-79 VGPRs, where that
+    // costs a wave per SIMD or shifts their register assignment (-5 to -10 %,
+    // profiles/r02_ab_layouts/), so they read the claim in front of the chunk.
+    constexpr bool kDeferClaims = NBLK == 1;
     uint32_t x = (blockIdx.x - 1u) % kClaimCounters;
     const bool skip = stop != 0u || global_of_local(L.i_begin, L.rbits, L.base_tb) >= best;
-#if DPOW_STATIC_FIRST
-    const uint64_t cbase = L.n_static;
-    const uint32_t wave_id = __builtin_amdgcn_readfirstlane((blockIdx.x - 1u) * (kBlockThreads / 64) + threadIdx.x / 64u);
-    uint64_t claim = skip ? L.n_chunks
-                          : (wave_id < cbase ? (uint64_t)wave_id : claim_next(L.claim + x * kClaimStride, x, lane, cbase));
-#else
-    constexpr uint64_t cbase = 0;
-    uint64_t claim = skip ? L.n_chunks : claim_next(L.claim + x * kClaimStride, x, lane, cbase);
-#endif
+    const uint64_t cbase = kStaticFirst ? L.n_static : 0;
+    uint64_t claim;
+    if constexpr (kStaticFirst) {
+        const uint32_t wave_id =
+            __builtin_amdgcn_readfirstlane((blockIdx.x - 1u) * (kBlockThreads / 64) + threadIdx.x / 64u);
+        claim = skip ? L.n_chunks
+                     : (wave_id < cbase ? (uint64_t)wave_id : claim_next(L.claim + x * kClaimStride, x, lane, cbase));
+    } else {
+        claim = skip ? L.n_chunks : claim_next(L.claim + x * kClaimStride, x, lane, cbase);
+    }
 #if DPOW_WAVE_TRACE
     t_first = __builtin_amdgcn_s_memrealtime() + (claim & 0);
 #endif
     uint32_t hops = 0;
     for (;;) {
-#if DPOW_STEAL
         // This counter is drained: move on to the next one (its waves may sit
         // on a slower XCD).  A counter only ever drains, so after a full round
         // of drained counters every chunk has been handed out.
@@ -1214,34 +958,18 @@ DPOW_DEV void search_body(const Launch &L) {
                         : L.n_chunks;
             continue;
         }
-#else
-        if (claim >= L.n_chunks) break;
-#endif
-#if DPOW_CLAIM_AHEAD
-        // With kDeferClaims the next claim's atomic is issued now and its result read after
-        // this chunk (claim_take): the wave hashes while the atomic is in flight.
+        // kDeferClaims: the next claim's atomic is issued in the chunk's last group and its
+        // result read after the chunk (claim_take); else the next claim is taken now.
         unsigned long long next_v = 0;
         uint64_t next = 0;
-        bool issued = false;  // kLate: the next claim's atomic was issued (in the chunk's last group)
-        if constexpr (kLate) (void)issued;
-        else if constexpr (kDeferClaims) next_v = claim_issue<true>(L.claim + x * kClaimStride, lane);
+        bool issued = false;  // kDeferClaims: the next claim's atomic was issued (in the chunk's last group)
+        if constexpr (kDeferClaims) (void)issued;
         else next = claim_next(L.claim + x * kClaimStride, x, lane, cbase);
-#endif
         // Claims [0, n_big) are `chunk` wave-blocks, the rest `chunk_tail`: the
         // launch ends on small claims, so its waves run dry within a few
         // wave-blocks of each other (the tail of a 2.5 ms launch was ~3 %).
         const bool big = claim < L.n_big;
-#if DPOW_TAIL_PRIO
-#if DPOW_HEAD_PRIO
-        // Head priority: the two claims every wave takes at its start are the
-        // launch's lowest chunks; a young wave hashes them at priority 2, so a
-        // first hit beyond them does not wait for the launch to drain.
         if (!big) __builtin_amdgcn_s_setprio(0);
-        else if (claim >= L.n_head) __builtin_amdgcn_s_setprio(1);
-#else
-        if (!big) __builtin_amdgcn_s_setprio(0);
-#endif
-#endif
         const uint64_t b_begin = big ? claim * L.chunk : L.n_big * L.chunk + (claim - L.n_big) * L.chunk_tail;
         const uint32_t csz = big ? L.chunk : L.chunk_tail;
         const uint32_t nb = (uint32_t)(b_begin + csz < L.n_wblocks ? csz : L.n_wblocks - b_begin);
@@ -1260,7 +988,6 @@ DPOW_DEV void search_body(const Launch &L) {
         t_last = __builtin_amdgcn_s_memrealtime();
         c_last = claim;
 #endif
-#if DPOW_POLL_WB > 0
         // The chunk runs in groups of L.poll_wb wave-blocks.  Each group's loads of
         // Ctrl::best / Ctrl::stop are issued before it and consumed after it (the
         // latency hides behind the hashing), so a hit elsewhere or a cancel ends
@@ -1273,8 +1000,6 @@ DPOW_DEV void search_body(const Launch &L) {
         const uint32_t poll_wb = kLaunchPoll<NBLK, W0, SH> ? L.poll_wb : (uint32_t)DPOW_POLL_WB;
         for (;;) {
             uint32_t q = left < poll_wb ? left : poll_wb;
-            [[maybe_unused]] const uint32_t q0 = q;  // (kFair: wave-blocks of this group)
-#if DPOW_SPAN
             // A chunk never straddles a 2^24-k segment boundary (the host aligns a
             // spanning launch's chunks to them, dpow_api.cpp), so neither does a
             // group; entering another segment re-derives the segment words' K + M
@@ -1292,16 +1017,13 @@ DPOW_DEV void search_body(const Launch &L) {
                     if constexpr (SH == 0) lov = lane_offset(L.rbits, lane) + d0;
                 }
             }
-#endif
             left -= q;
-#if DPOW_CLAIM_AHEAD
-            if constexpr (kLate) {
+            if constexpr (kDeferClaims) {
                 if (left == 0) {  // the chunk's last group: reserve the next chunk now
                     next_v = claim_issue<true>(L.claim + x * kClaimStride, lane);
                     issued = true;
                 }
             }
-#endif
             const unsigned long long best_seen =
                 __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t stop_seen = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1322,44 +1044,9 @@ DPOW_DEV void search_body(const Launch &L) {
             }
             best = best_seen < best ? best_seen : best;
             stop = stop_seen;
-            if constexpr (kFair) {
-                // behind a fair share of the device since this wave started: priority 2 (big claims;
-                // the tail's claims stay at 0, tail priority)
-                const uint32_t done_wb = __builtin_amdgcn_readfirstlane(fair_wb_v) + (q0 - q);
-                asm volatile("v_mov_b32 %0, %1" : "=v"(fair_wb_v) : "s"(done_wb));
-                const uint32_t el = (uint32_t)__builtin_amdgcn_s_memrealtime() - __builtin_amdgcn_readfirstlane(fair_t0_v);
-                if (claim < L.n_big) {
-                    if (el > (done_wb + 2u) * L.fair_ticks) __builtin_amdgcn_s_setprio(2);
-                    else __builtin_amdgcn_s_setprio(1);
-                }
-            }
             if (hit || left == 0 || stop != 0u || global_of_local(i0, L.rbits, L.base_tb) >= best) break;
         }
-#else
-        // Issued now, consumed at the next claim: the latency hides behind the chunk.
-        const unsigned long long best_next =
-            __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t stop_next = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // A hit ends the chunk: its later wave-blocks hold larger indices.
-        uint64_t i0 = i_first;
-        for (uint32_t r = 0; r < nb; ++r, i0 += (uint64_t)kWaveBlock) {
-            const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, kc, i0, lane, loff);
-            if (g != kNoHitG) {
-                best = g < best ? g : best;
-                break;
-            }
-        }
-        best = best_next < best ? best_next : best;
-        stop = stop_next;
-#endif
-        if constexpr (kFresh) {
-            const unsigned long long bf = __hip_atomic_load(&L.ctrl->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t sf = __hip_atomic_load(&L.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            best = bf < best ? bf : best;
-            stop |= sf;
-        }
-#if DPOW_CLAIM_AHEAD
-        if constexpr (kLate) {
+        if constexpr (kDeferClaims) {
             // left the chunk before its last group (a hit, a bound, a stop): every later chunk
             // is at or above the best, or the launch is stopping -- nothing more to claim
             if (!issued) {
@@ -1369,15 +1056,9 @@ DPOW_DEV void search_body(const Launch &L) {
                 break;
             }
             claim = claim_take(next_v, x, cbase);
-        } else if constexpr (kDeferClaims) {
-            claim = claim_take(next_v, x, cbase);
         } else {
             claim = next;
         }
-#else
-        if (stop != 0u) break;
-        claim = claim_next(L.claim + x * kClaimStride, x, lane, cbase);
-#endif
     }
     // Retirement is counted per workgroup (a quarter of the atomics on the
     // shared counter).  Each wave's atomicMin has been performed already (the
@@ -1417,52 +1098,43 @@ DPOW_DEV void search_body(const Launch &L) {
 #if DPOW_WAVE_TRACE
         const unsigned long long t_bar = __builtin_amdgcn_s_memrealtime();
 #endif
-#if DPOW_XCD_RETIRE == 2
+        if constexpr (kXcdRetire) {
+            // Retirement is counted per claim counter first (worker block b serves counter
+            // (b - 1) % 8, its XCD's) on a word of that counter's line, and the counter's last
+            // workgroup adds the counter's count to Ctrl::done: a launch's few hundred to ~1500
+            // retirements no longer queue on one line (~100 atomics per us) at its end.
+            const uint32_t n_wg = gridDim.x - 1u;
+            const uint32_t xr = (blockIdx.x - 1u) % kClaimCounters;
+            const uint32_t nx = n_wg / kClaimCounters + (xr < n_wg % kClaimCounters ? 1u : 0u);
+            unsigned long long *const xc = L.claim + xr * kClaimStride + 2;
+            const unsigned long long px = __hip_atomic_fetch_add(xc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (px + 1ull == (unsigned long long)nx) {
+                // every retirement of this counter is in: zero it for the slot's next launch
+                __hip_atomic_store(xc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if DPOW_WAVE_TRACE
-        {
-            unsigned long long *r = g_wave_trace + kTraceFields * (kTraceWaves - 2);
-            r[0] = t_claims;  // (every workgroup writes; the publisher's retire() writes r[2] last)
-            r[1] = t_bar;
-        }
+                if (prev + nx == L.done_target) {  // the publisher's retirement: slot kTraceWaves - 2
+                    unsigned long long *r = g_wave_trace + kTraceFields * (kTraceWaves - 2);
+                    r[0] = t_claims;
+                    r[1] = t_bar;
+                    r[2] = __builtin_amdgcn_s_memrealtime() + (prev & 0);
+                }
 #endif
-        retire(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr, L.done_target);
-#elif DPOW_XCD_RETIRE
-        // Retirement is counted per claim counter first (worker block b serves counter
-        // (b - 1) % 8, its XCD's) on a word of that counter's line, and the counter's last
-        // workgroup adds the counter's count to Ctrl::done: a launch's few hundred to ~1500
-        // retirements no longer queue on one line (~100 atomics per us) at its end.
-        const uint32_t n_wg = gridDim.x - 1u;
-        const uint32_t xr = (blockIdx.x - 1u) % kClaimCounters;
-        const uint32_t nx = n_wg / kClaimCounters + (xr < n_wg % kClaimCounters ? 1u : 0u);
-        unsigned long long *const xc = L.claim + xr * kClaimStride + 2;
-        const unsigned long long px = __hip_atomic_fetch_add(xc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (px + 1ull == (unsigned long long)nx) {
-            // every retirement of this counter is in: zero it for the slot's next launch
-            __hip_atomic_store(xc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (prev + nx == L.done_target)
+                    publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
+            }
+        } else {
+            const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if DPOW_WAVE_TRACE
-            if (prev + nx == L.done_target) {  // the publisher's retirement: slot kTraceWaves - 2
+            if (prev + 1u == L.done_target) {  // the publisher's retirement: slot kTraceWaves - 2
                 unsigned long long *r = g_wave_trace + kTraceFields * (kTraceWaves - 2);
                 r[0] = t_claims;
                 r[1] = t_bar;
                 r[2] = __builtin_amdgcn_s_memrealtime() + (prev & 0);
             }
 #endif
-            if (prev + nx == L.done_target)
-                publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
+            if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
         }
-#else
-        const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if DPOW_WAVE_TRACE
-        if (prev + 1u == L.done_target) {  // the publisher's retirement: slot kTraceWaves - 2
-            unsigned long long *r = g_wave_trace + kTraceFields * (kTraceWaves - 2);
-            r[0] = t_claims;
-            r[1] = t_bar;
-            r[2] = __builtin_amdgcn_s_memrealtime() + (prev & 0);
-        }
-#endif
-        if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
-#endif
     }
 }
 

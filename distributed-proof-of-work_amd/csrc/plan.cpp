@@ -32,7 +32,6 @@ uint32_t chunk_len_of(uint64_t k) {
 uint64_t segment_end(uint64_t k) {
     const uint32_t L = chunk_len_of(k);
     if (L == 0) return 1;
-    if (!DPOW_SPAN && L >= 4) return ((k >> 24) + 1) << 24;
     return 1ull << (8 * L);
 }
 
@@ -107,7 +106,7 @@ uint64_t lspan_end(size_t nonce_len, uint32_t rbits, uint32_t ntz) {
     // a launch (k < 2^16, 2^16 R candidates): their two launches cost 17 + 122 us against
     // 77 us of hashing (profiles/r03_tts_timeline_c.json, [1,2,3,4]/8).
     // Returns the k below which launches use the chunk-length-0 template (0: none).
-    if (!(DPOW_LSPAN && nonce_len % 4 == 0 && rbits >= 1)) return 0;
+    if (!(nonce_len % 4 == 0 && rbits >= 1)) return 0;
     return expected_first_hit(ntz, rbits) <= kLspanMaxExpect ? 1ull << 24 : 1ull << 16;
 }
 
@@ -132,7 +131,7 @@ bool WindowPlanner::next(PlannedLaunch &pl) {
     if (cap_end < ke) ke = cap_end;
     const uint32_t L = chunk_len_of(k);
     const uint32_t nblk = nblk_of(L);
-    pl.k0 = DPOW_START_K0 && k == 0;
+    pl.k0 = k == 0;
     // (the k = 0 kernel hashes k = 0 from the real chunk-length-0 template: no deltas)
     uint32_t L_last = L;
     if (!pl.k0 && k >= 1 && lseg_template(k)) {
@@ -227,7 +226,7 @@ void candidate_words(const PlannedLaunch &pl, uint64_t local_idx, uint32_t words
         words[w0 + 1] += d1;
         words[lenw] += dlen;
     }
-    if (DPOW_SPAN) {  // the segment words, as the kernel re-derives them (md5_search_kernel.h seg_word)
+    {  // the segment words, as the kernel re-derives them (md5_search_kernel.h seg_word)
         uint32_t d1, d2;
         const uint32_t seg = (uint32_t)((local_idx >> Lh.rbits) >> 24);
         seg_word_deltas(Lh.T[w0 + 1], Lh.T[w0 + 2], seg, Lh.seg_first, sh, d1, d2);
@@ -262,7 +261,7 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
     uint64_t chunk = span_wb / (worker_blocks * wpb * claims_per_wave);
     if (chunk < min_chunk) chunk = min_chunk;
     if (chunk > kMaxChunk) chunk = kMaxChunk;
-    if ((DPOW_SPAN && (pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24)) || L.lspan) {
+    if ((pl.info.k_begin >> 24) != ((pl.info.k_end - 1) >> 24) || L.lspan) {
         // The launch spans 2^24-k segments: a power-of-two chunk and wave-blocks
         // counted from a multiple of chunk wave-blocks put every segment boundary
         // (a multiple of 2^24 * R indices) on a claim boundary, big or tail, so no
@@ -300,11 +299,11 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
     L.n_big = n_big;
     L.n_chunks = n_chunks;
     L.n_head = 2 * worker_blocks * wpb;
-    // Static first claims (md5_search_kernel.h DPOW_STATIC_FIRST): the "_ls" kernels (the
+    // Static first claims (md5_search_kernel.h kStaticFirst): the "_ls" kernels (the
     // chunk-length-0 template, L.seg0 == kLsegBase) hand claim w to worker wave w.  Every
     // counter that holds a claim beyond them still has a workgroup (checked above on
     // n_chunks, which bounds the counters' share too).
-    L.n_static = DPOW_STATIC_FIRST_HOST && L.seg0 == kLsegBase && !pl.k0
+    L.n_static = L.seg0 == kLsegBase && !pl.k0
                      ? (n_chunks < worker_blocks * wpb ? n_chunks : worker_blocks * wpb)
                      : 0;
     *worker_blocks_out = worker_blocks;
@@ -314,9 +313,9 @@ int size_launch(PlannedLaunch &pl, uint64_t max_blocks, uint64_t expect, uint64_
 uint32_t launch_poll_wb(uint32_t ntz, uint32_t rbits) {
     const uint32_t slow = DPOW_POLL_WB > 0 ? DPOW_POLL_WB : 16;
     const uint64_t expect = expected_first_hit(ntz, rbits);
-    if (DPOW_SMALL_GRIDS && expect <= kTinyExpect) return 1;
-    if (DPOW_SMALL_GRIDS && expect <= kNearExpect) return kNearPollWb;
-    if (DPOW_SMALL_GRIDS && expect <= kMidExpect) return kMidPollWb;
+    if (expect <= kTinyExpect) return 1;
+    if (expect <= kNearExpect) return kNearPollWb;
+    if (expect <= kMidExpect) return kMidPollWb;
     return expect <= kFastPollCands ? kFastPollWb : slow;
 }
 
@@ -326,8 +325,8 @@ uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits) {
 
 uint64_t launch_min_chunk(uint32_t ntz, uint32_t rbits) {
     const uint64_t expect = expected_first_hit(ntz, rbits);
-    if (DPOW_SMALL_GRIDS && expect <= kTinyExpect) return kTinyChunk;
-    return DPOW_SMALL_GRIDS && expect > kMidChunkExpect && expect <= kMidExpect ? kMidChunk : kMinChunk;
+    if (expect <= kTinyExpect) return kTinyChunk;
+    return expect > kMidChunkExpect && expect <= kMidExpect ? kMidChunk : kMinChunk;
 }
 
 int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t share, const LaunchKnobs &knobs,
@@ -342,11 +341,6 @@ int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t s
                                knobs.cpw ? knobs.cpw : launch_claims_per_wave(ntz, L.rbits));
     if (rc < 0) return rc;
     L.poll_wb = knobs.poll_wb ? knobs.poll_wb : launch_poll_wb(ntz, L.rbits);
-    // Fair priority (md5_search_kernel.h DPOW_FAIR_PRIO): s_memrealtime ticks (100 MHz) per
-    // wave-block of a wave at a fair share of the device -- waves x 128 candidates / kFairRate --
-    // with 25 % slack.
-    const double waves = (double)*worker_blocks * (kBlockThreads / 64);
-    L.fair_ticks = (uint32_t)std::max(1.0, 1.25 * waves * (double)kWaveBlock / kFairRate * 1e8);
     return 0;
 }
 
@@ -366,8 +360,7 @@ bool cap_shared_launch(WindowPlanner &planner, PlannedLaunch &pl, uint64_t activ
 }
 
 uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits, uint64_t share) {
-#if DPOW_SMALL_GRIDS
-    // Candidates of this partition expected before its first hit: 16^N R / 256, and the
+    // Small grids for short launches: candidates of this partition expected before its first hit: 16^N R / 256, and the
     // launch's, in device time (times the searches sharing the device; saturating).
     const auto dev = [share](uint64_t v) { return share > 1 && v > ~0ull / share ? ~0ull : v * (share ? share : 1); };
     const uint64_t expect = dev(expected_first_hit(ntz, rbits));
@@ -376,9 +369,6 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits,
     if (eff <= (1ull << 22)) return kMaxBlocksPerCu < 3 ? kMaxBlocksPerCu : 3;
     if (eff <= kMidExpect) return kMaxBlocksPerCu < 4 ? kMaxBlocksPerCu : 4;
     if (kFiveExpect && expect <= kFiveExpect) return kMaxBlocksPerCu < 5 ? kMaxBlocksPerCu : 5;
-#else
-    (void)candidates, (void)ntz, (void)rbits, (void)share;
-#endif
     return kMaxBlocksPerCu;
 }
 

@@ -27,13 +27,6 @@ uint64_t word2_period(uint32_t sh);
 // layouts, R >= 2, equal block counts (WindowPlanner::next).
 constexpr uint64_t kLspanMaxExpect = 1ull << 28;
 uint64_t lspan_end(size_t nonce_len, uint32_t rbits, uint32_t ntz);
-#ifndef DPOW_START_K0
-#define DPOW_START_K0 1  // k = 0 hashed by the search's k = 0 kernel (A/B switch)
-#endif
-#ifndef DPOW_STATIC_FIRST_HOST
-#define DPOW_STATIC_FIRST_HOST 1  // static first claims in the "_ls" kernels (A/B switch; the kernels'
-                                  // DPOW_STATIC_FIRST must match: both read Launch::n_static)
-#endif
 uint32_t remainder_bits(uint32_t worker_bits);
 uint32_t base_thread_byte(uint32_t worker_byte, uint32_t worker_bits);
 
@@ -203,9 +196,6 @@ uint64_t launch_claims_per_wave(uint32_t ntz, uint32_t rbits);
 #ifndef DPOW_BLOCKS_PER_CU
 #define DPOW_BLOCKS_PER_CU 6
 #endif
-#ifndef DPOW_SMALL_GRIDS
-#define DPOW_SMALL_GRIDS 1  // fewer workgroups per CU for short launches (A/B switch)
-#endif
 constexpr uint64_t kMaxBlocksPerCu = DPOW_BLOCKS_PER_CU;
 // share: searches in flight on the device (dpow_api.cpp g_active).  Such a search runs at
 // 1/share of the device, so the tiers judge its launch by device time: candidates and the
@@ -219,7 +209,6 @@ uint64_t launch_blocks_per_cu(uint64_t candidates, uint32_t ntz, uint32_t rbits,
 // counter), size_launch with the ntz-dependent expected first hit, minimum chunk and
 // claims per wave, and the poll group (L.poll_wb).  Non-zero knobs override the policy
 // (the DPOW_DIAG_* A/B environment of dpow_open).
-constexpr double kFairRate = 2.05e11;  // candidates/s of a device at 4-6 workgroups per CU (one block)
 struct LaunchKnobs {
     uint32_t bpc = 0, min_chunk = 0, cpw = 0, poll_wb = 0;
     uint32_t share_launch_us = 0;  // launch length on a shared device (kShareLaunchNs)

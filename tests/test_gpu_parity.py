@@ -418,7 +418,7 @@ def _all_hits(miner, nonce, ntz, wb, wbits, k0, k1, cap=2000):
     (4, (1 << 55) - 1 - (3 << 24) - 100, 3),                  # the top of the k range
 ])
 def test_spanning_launch_equals_per_segment_windows(miner, oracle, nlen, first_k, nseg):
-    """The segment-word path (DPOW_SPAN): one search over a window spanning nseg 2^24-k
+    """The segment-word path (launches spanning 2^24-k segments): one search over a window spanning nseg 2^24-k
     segments from an unaligned k finds exactly the hits that searches confined to one
     segment each find (there the template holds the segment's own k >> 24 bytes), and
     the first one agrees with the byte-wise oracle on the 4096 k before it."""

@@ -51,7 +51,7 @@ def test_hash_block_instruction_mix(kernel_110):
 def test_pipeline_order_and_padding(kernel_110):
     _, lines = kernel_110
     seq = _kinds(lines).replace(".", "")
-    # one padded step pair in DPOW_PIPE_ORDER 2: p.B q.R p.A q.D p.R q.B p.D q.A
+    # one padded step pair (md5_search_kernel.h DPOW_PIPE_BODY): p.B q.R p.A q.D p.R q.B p.D q.A
     # = F H H F H F F H, each rotate and add3 followed by its s_nop
     group = "FHnHnFHnFFHn"
     assert seq.count(group) >= 50, seq[:400]
@@ -61,7 +61,7 @@ def test_pipeline_order_and_padding(kernel_110):
 
 
 def test_claim_ahead_latency_hidden(kernel_110):
-    """The claim requested ahead of a chunk (md5_search_kernel.h, DPOW_CLAIM_DEFER) is read
+    """The claim requested ahead of a chunk (md5_search_kernel.h, kDeferClaims) is read
     after the chunk: its atomic precedes the hash block and the readfirstlane of its
     result follows it, so the wave hashes while the atomic is in flight.  (On a uniform
     address the AMDGPU atomic optimizer would rewrite the atomic into a wave reduction that
@@ -91,7 +91,7 @@ def test_sweep_kernel_hash_block_placement():
     """The sweep's kernel (<1,1,0> with the D-equality test) keeps its hash block at round 4's
     offset modulo 256 (0x68): every watcher change re-runs the kernel's register allocation and
     moves its code, and a 4-16 byte move of the hash block alone cost the sweep 0.3-0.5 % in
-    round 5 (md5_search_kernel.h DPOW_PAD_4B restores the offset)."""
+    round 5 (md5_search_kernel.h kPad4B restores the offset)."""
     import isa_loop
     text = isa_loop.disasm(os.path.join(ROOT, "distributed-proof-of-work_amd", "csrc"), 1, 0, [])
     lines = isa_loop.kernel_lines(text, 1, 1, 0, 1)

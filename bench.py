@@ -699,10 +699,19 @@ def collective_probe(miner, rank, world, dev, board, backend, gpu, reps=200):
         tts[f"{bytes(nonce).hex()}/{n}"] = {"search_ms": round(sorted(ms)[len(ms) // 2], 3),
                                             "global_idx": res.global_idx, "batches": res.batches}
     med = lambda v: round(sorted(v)[len(v) // 2], 1)  # noqa: E731
+    boundary = {"median": med(lat), "p90": round(sorted(lat)[int(len(lat) * 0.9)], 1)}
     return {"backend": backend, "world": world, **({"ok": False, "wrong": wrong} if wrong else {}),
-            "batch_boundary_us": {"median": med(lat), "p90": round(sorted(lat)[int(len(lat) * 0.9)], 1)},
+            "batch_boundary_us": boundary,
+            # The two batch boundaries side by side: the RCCL MIN all-reduce over
+            # xGMI (the process group's, with the nccl backend; ranks on different hosts take it), and
+            # the node vote through the shared board, which node_mine uses when every rank shares
+            # the host.  A gloo rehearsal has no RCCL path: its ranks share one GPU, and RCCL needs
+            # one GPU per rank.
+            "rccl_boundary_us": (boundary if backend == "nccl" else
+                                 {"skipped": "backend gloo (a rehearsal on one GPU: RCCL needs a GPU per rank)"}),
             "node_vote_us": ({"median": med(vote), "p90": round(sorted(vote)[int(len(vote) * 0.9)], 1)}
                              if vote else None),
+            "node_boundary": "node vote (shared board)" if vote else f"{backend} all-reduce",
             "batch_2p16_candidates_us": {"median": med(batch), "p90": round(sorted(batch)[int(len(batch) * 0.9)], 1)},
             "node_mine": tts}
 

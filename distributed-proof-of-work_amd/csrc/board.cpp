@@ -261,8 +261,10 @@ int dpow_board_search(dpow_board *b, dpow_ctx *ctx, const uint8_t *nonce, size_t
     uint64_t epoch = 0;  // the entry's votes start at zero (board_join)
     uint32_t batches = 0;
     const uint64_t batch_k = kBatchCandidates >> (8 - worker_bits);
+    dpow::set_solo(ctx, role == 1);
     rc = dpow::node_mine(ctx, slot, e->votes, worker_byte, world, &epoch, kVoteTimeoutNs, nonce, nonce_len, ntz, 0,
                          DPOW_K_LIMIT, 0, batch_k, best_global_idx, secret_out, secret_len, &batches, true, role);
+    dpow::set_solo(ctx, false);
     const std::string err = rc < 0 ? dpow_last_error() : "";
     (void)dpow_board_leave(b, slot);
     if (rc < 0) return dpow::fail(rc, err.c_str());

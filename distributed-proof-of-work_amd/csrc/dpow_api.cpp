@@ -142,9 +142,11 @@ constexpr int64_t kEstFixedNs = 8000;
 // every search's grid follows the others that start or end beside it.
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_active[kMaxDevices];
-// Contexts open per device in this process: more than one means other searches may start
-// beside this one at any moment (a worker pool, the coordinator mirror's logical workers).
-std::atomic<int> g_open[kMaxDevices];
+// Contexts open per device in this process, each with the time it was last used (opened, or a
+// search started): several used recently means other searches may start beside this one at any
+// moment (the coordinator mirror's logical workers); contexts idle in a pool do not count.
+std::mutex g_ctx_mu;
+std::vector<dpow_ctx *> g_ctxs;
 
 struct ActiveSearch {
     int dev;
@@ -210,7 +212,7 @@ struct SearchWait {
 
 struct dpow_ctx {
     int device = 0;
-    bool counted = false;  // in g_open
+    bool counted = false;  // in g_ctxs
     hipStream_t stream = nullptr;
     Ctrl *d_ctrl = nullptr;  // kCtrlRing control blocks (kCtrlStride apart, aligned to the ring's size);
                              //  ctrl_idx's is clean
@@ -254,6 +256,8 @@ struct dpow_ctx {
     size_t diag_nl = 0;
     int64_t diag_t0 = 0;
     uint64_t dev_key = 0;  // the GPU's identity across processes: a hash of its PCI bus id (dpow::device_key)
+    std::atomic<int64_t> last_use{0};  // now_ns() of dpow_open / the last search start (recent_contexts)
+    bool solo = false;  // dpow_board_search's node-wide role: no young-search sharing (plan.h kYoungNs)
 };
 
 namespace {
@@ -380,6 +384,16 @@ int retire_slot(dpow_ctx *c, LaunchSlot &s) {
     }
     s.in_flight = false;
     return 0;
+}
+
+// Contexts of `device` used within kRecentNs (the young-search rule above).
+int recent_contexts(int device) {
+    const int64_t t = now_ns();
+    int n = 0;
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    for (dpow_ctx *x : g_ctxs)
+        if (x->device == device && t - x->last_use.load(std::memory_order_relaxed) < kRecentNs) ++n;
+    return n;
 }
 
 // The body of dpow_search (arguments checked).
@@ -605,13 +619,13 @@ int search_window(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t 
         // This search's share of the device's resident workgroups (searches sharing the device:
         // plan.h grid_share, cap_shared_launch).
         uint64_t active = (uint64_t)std::max(1, g_active[c->device].load(std::memory_order_relaxed));
-        if (active == 1 && now_ns() - sw.t0 < kYoungNs) {
-            // A young search that looks alone while other contexts of this process are open on
-            // the device plans as if they all searched: its first long launch no longer takes
-            // the whole device for its full length just because it registered first (round 4:
-            // one 16-28 ms full-device launch, config 4's one nonce 8.5-23 ms over runs).
-            const int open = g_open[c->device].load(std::memory_order_relaxed);
-            if (open > 1) active = (uint64_t)open;
+        if (active == 1 && !c->solo && now_ns() - sw.t0 < kYoungNs) {
+            // A young search that looks alone while other contexts of this process were used on
+            // the device recently plans as if they all searched: its first long launch no longer
+            // takes the whole device for its full length just because it registered first
+            // (round 4: one 16-28 ms full-device launch, config 4's one nonce 8.5-23 ms over runs).
+            const int recent = recent_contexts(c->device);
+            if (recent > 1) active = (uint64_t)recent;
         }
         const uint64_t share = grid_share(active, c->knobs);
         cap_shared_launch(planner, pl, active, c->knobs);
@@ -842,8 +856,10 @@ int dpow_open(int device, dpow_ctx **out) {
         dpow_close(c);
         return hip_fail(e, "dpow_open: loading the search kernels");
     }
-    if (device < kMaxDevices) {
-        g_open[device].fetch_add(1, std::memory_order_relaxed);
+    c->last_use.store(now_ns(), std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(g_ctx_mu);
+        g_ctxs.push_back(c);
         c->counted = true;
     }
     *out = c;
@@ -852,7 +868,10 @@ int dpow_open(int device, dpow_ctx **out) {
 
 void dpow_close(dpow_ctx *c) {
     if (!c) return;
-    if (c->counted) g_open[c->device].fetch_sub(1, std::memory_order_relaxed);
+    if (c->counted) {
+        std::lock_guard<std::mutex> g(g_ctx_mu);
+        g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), c), g_ctxs.end());
+    }
     const DeviceScope on_device(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     // Drained: no watcher of ours reads the node pages any more.  Leave the page registry
@@ -1139,6 +1158,10 @@ int dpow::node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *vot
 int dpow::fail(int code, const char *msg) { return set_error(code, msg); }
 
 uint64_t dpow::device_key(const dpow_ctx *c) { return c ? c->dev_key : 0; }
+
+void dpow::set_solo(dpow_ctx *c, bool solo) {
+    if (c) c->solo = solo;
+}
 
 extern "C" {
 
@@ -1522,6 +1545,7 @@ int dpow_search(dpow_ctx *c, const uint8_t *nonce, size_t nonce_len, uint32_t nt
     if (k_end > DPOW_K_LIMIT) return set_error(DPOW_ERANGE, "dpow_search: k_end beyond DPOW_K_LIMIT");
     *secret_len = 0;
     c->stats.searches++;
+    c->last_use.store(now_ns(), std::memory_order_relaxed);
     if (k_begin >= k_end) return DPOW_EXHAUSTED;
     // A node slot whose stop is raised (another rank was cancelled or failed), or a
     // raised cancel flag: nothing to do.  A node slot's stop is raised by every

@@ -25,6 +25,10 @@ int node_mine(dpow_ctx *c, dpow_node_slot *slot, dpow_node_vote_entry *votes, ui
 // The GPU of ctx across the processes of a host (a hash of its PCI bus id, never 0).
 uint64_t device_key(const dpow_ctx *c);
 
+// The context searches every partition of a node whose ranks share its GPU (dpow_board_search):
+// the young-search rule (plan.h kYoungNs) does not share the device with the idle ranks.
+void set_solo(dpow_ctx *c, bool solo);
+
 // Sets dpow_last_error for the calling thread and returns code.
 int fail(int code, const char *msg);
 

@@ -242,15 +242,18 @@ int size_search_launch(PlannedLaunch &pl, uint32_t ntz, uint64_t cus, uint64_t s
 #endif
 constexpr uint64_t kShareMax = DPOW_SHARE_MAX;
 // A search younger than kYoungNs that is alone on its device while other contexts of its
-// process are open there plans its launches for all of them (dpow_api.cpp g_open): searches
-// that start together -- the coordinator mirror's workers -- then share the device from their
-// first launch, instead of the first to register taking one uncapped full-device launch
-// (round 4).  A process with one context per device (a node rank, the bench)
-// is unaffected.
+// process were used there within kRecentNs (opened, or a search started: dpow_api.cpp
+// recent_contexts) plans its launches for all of them: searches that start together -- the
+// coordinator mirror's workers -- then share the device from their first launch, instead of
+// the first to register taking one uncapped full-device launch (round 4).  Contexts idle in a
+// pool for longer do not count, nor does the rank that searches a whole node's
+// window on a shared GPU (dpow_board_search: its co-located ranks only vote).  A process with
+// one context per device (a node rank, the bench) is unaffected.
 #ifndef DPOW_YOUNG_US
 #define DPOW_YOUNG_US 2000
 #endif
 constexpr int64_t kYoungNs = (int64_t)DPOW_YOUNG_US * 1000;
+constexpr int64_t kRecentNs = 100 * 1000 * 1000;
 constexpr int64_t kShareLaunchNs = (int64_t)DPOW_SHARE_LAUNCH_US * 1000;
 constexpr double kEstRate = 2.3e11;  // candidates/s of one device (bench: 217-218 on the one-block layouts)
 uint64_t grid_share(uint64_t active, const LaunchKnobs &knobs);

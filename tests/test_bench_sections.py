@@ -125,3 +125,17 @@ def test_stdout_carries_only_the_json_line():
     assert r.stdout.splitlines() == ['{"metric": "m", "value": 1}'], r.stdout
     assert "RCCL version" in r.stderr and "a python print" in r.stderr
 
+
+def test_collective_reports_both_boundaries():
+    """at N > 1 the collective section carries the RCCL boundary next to the
+    node vote, and says which one node_mine uses.  A gloo rehearsal (two CPU ranks here) marks the
+    RCCL entry skipped and measures the vote through the shared board."""
+    outs, _ = _ranks(2, [], BENCH_ARGS)
+    (rc0, out0, err0), (rc1, _, err1) = outs
+    assert rc0 == 0 and rc1 == 0, (err0[-3000:], err1[-3000:])
+    col = _line(out0)["collective"]
+    assert col["world"] == 2 and col["backend"] == "gloo"
+    assert "skipped" in col["rccl_boundary_us"]
+    assert col["node_vote_us"]["median"] > 0 and col["batch_boundary_us"]["median"] > 0
+    assert col["node_boundary"] == "node vote (shared board)"
+

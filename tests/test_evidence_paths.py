@@ -12,7 +12,7 @@ import os
 import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOCS = ["DESIGN.md", "README.md", "INTEGRATION.md"]
+DOCS = ["DESIGN.md", "DESIGN_HISTORY.md", "README.md", "INTEGRATION.md"]
 
 
 def citations():

@@ -33,7 +33,7 @@ def _cases(seed=20261018, count=10):
     return [([rng.randrange(256) for _ in range(4)], rng.choice((4, 5)), rng.choice((2, 4))) for _ in range(count)]
 
 
-def test_native_rank_search_with_posts_vs_oracle(oracle):
+def _posts_vs_oracle(oracle, cases, k_end, delays_us=(0, 60)):
     import distpow
     from distpow.node import NodeBoard, node_mine
 
@@ -42,15 +42,15 @@ def test_native_rank_search_with_posts_vs_oracle(oracle):
     checked = 0
     try:
         with distpow.Miner(0) as m:
-            for nonce, ntz, world in _cases():
+            for nonce, ntz, world in cases:
                 b = world.bit_length() - 1
-                k_end = 1 << 20  # the oracle stops at the first hit (16^N / R k expected)
                 g = oracle.mine_window(nonce, ntz, 0, 0, 0, k_end)[1]
                 for rank in range(world):
                     hit = oracle.mine_window(nonce, ntz, rank, b, 0, k_end)
                     assert hit is not None
                     h = hit[1]
-                    for post, delay_us in ((g, random.randrange(0, 60)), (h + random.randrange(1, 1 << 20), 5)):
+                    for post, delay_us in ((g, random.randrange(*delays_us)),
+                                           (h + random.randrange(1, 1 << 20), random.randrange(*delays_us))):
                         slot = board.begin()
                         L.dpow_diag_node_post_at(slot, post, time.perf_counter_ns() + delay_us * 1000)
                         r = node_mine(None, nonce, ntz, rank, world, board=board, miner=m)
@@ -65,7 +65,24 @@ def test_native_rank_search_with_posts_vs_oracle(oracle):
                         checked += 1
     finally:
         board.close()
-    assert checked >= 40
+    return checked
+
+
+def test_native_rank_search_with_posts_vs_oracle(oracle):
+    # k_end: the oracle stops at the first hit (16^N / R k expected)
+    assert _posts_vs_oracle(oracle, _cases(), 1 << 20, (0, 60)) >= 40
+
+
+def test_native_rank_search_posts_across_launches_vs_oracle(oracle):
+    """the coverage exit (a post at or below what the consumed launches cover ends a
+    search) where a rank's window runs several launches, queued kDepth ahead, when the post
+    lands: 5- and 7-byte nonces (no chunk-length-spanning launch: the window splits at k = 256
+    and 65536, and each rank's first hit lies past k = 256), N = 5, world 2 and 4, the node's true
+    first hit and bogus posts above a rank's own first hit at random moments of its search."""
+    rng = random.Random(20261019)
+    cases = [([rng.randrange(256) for _ in range(nlen)], 5, world)
+             for world in (2, 4) for nlen in (5, 7) for _ in range(2)]
+    assert _posts_vs_oracle(oracle, cases, 1 << 20, (0, 80)) >= 48
 
 
 def test_search_returns_at_covered_bound_vs_oracle(oracle):

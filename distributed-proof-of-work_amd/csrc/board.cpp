@@ -16,7 +16,8 @@
 // Layout (all-zero is a valid empty board, so a freshly created shared-memory object needs no
 // initialiser and openers cannot race one): a 64-byte header (magic, lock) and kEntries task
 // entries.  Join and leave take the header's spin lock (a few hundred nanoseconds, once per
-// task and rank); the search itself never does.
+// task and rank; a lock held for 10 s -- a process that died inside -- is an error, not a
+// hang); the search itself never does.
 #include <errno.h>
 #include <stdlib.h>
 #include <fcntl.h>
@@ -79,23 +80,52 @@ struct Layout {
     Entry e[kEntries];
 };
 
+// The board's spin lock (join, leave, counters: a few hundred ns each).  A holder never blocks
+// inside it, so a wait of kLockTimeoutNs means a process died holding it: the caller then gets
+// DPOW_EPROTO instead of spinning forever.
+constexpr int64_t kLockTimeoutNs = 10ll * 1000000000ll;
+
+int64_t mono_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 class Lock {
    public:
     explicit Lock(uint32_t *w) : w_(w) {
+        int64_t t0 = 0;
         for (uint32_t it = 0;; ++it) {
             uint32_t z = 0;
-            if (__atomic_compare_exchange_n(w_, &z, 1u, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) return;
-            if (it % 64 == 63) sched_yield();
-            else __builtin_ia32_pause();
+            if (__atomic_compare_exchange_n(w_, &z, 1u, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) {
+                held_ = true;
+                return;
+            }
+            if (it % 64 != 63) {
+                __builtin_ia32_pause();
+                continue;
+            }
+            sched_yield();
+            const int64_t t = mono_ns();
+            if (!t0) t0 = t;
+            else if (t - t0 > kLockTimeoutNs) return;
         }
     }
-    ~Lock() { __atomic_store_n(w_, 0u, __ATOMIC_RELEASE); }
+    ~Lock() {
+        if (held_) __atomic_store_n(w_, 0u, __ATOMIC_RELEASE);
+    }
+    bool held() const { return held_; }
     Lock(const Lock &) = delete;
     Lock &operator=(const Lock &) = delete;
 
    private:
     uint32_t *w_;
+    bool held_ = false;
 };
+
+int lock_lost(const char *who) {
+    return dpow::fail(DPOW_EPROTO, (std::string(who) + ": the board's lock was held for 10 s (a worker process "
+                                                       "died inside a join or leave?)").c_str());
+}
 
 bool key_matches(const Entry &e, const uint8_t *nonce, size_t len, uint32_t ntz, uint32_t world) {
     return e.state == 1 && e.ntz == ntz && e.world == world && e.nonce_len == len &&
@@ -202,6 +232,7 @@ int dpow_board_leave(dpow_board *b, dpow_node_slot *slot) {
         return dpow::fail(DPOW_EINVAL, "dpow_board_leave: not a slot of this board");
     Entry &e = L.e[off / sizeof(Entry)];
     Lock lk(&L.h.lock);
+    if (!lk.held()) return lock_lost("dpow_board_leave");
     if (e.state != 1 || e.refs == 0) return dpow::fail(DPOW_EPROTO, "dpow_board_leave: the entry is not joined");
     // The last rank out frees the entry, whether or not every rank joined (a worker that
     // answered from its cache never does; the others left on their kill).
@@ -212,6 +243,7 @@ int dpow_board_leave(dpow_board *b, dpow_node_slot *slot) {
 int dpow_board_counters(dpow_board *b, uint64_t *tasks, uint64_t *shared_gpu) {
     if (!b || !b->mem || !tasks || !shared_gpu) return dpow::fail(DPOW_EINVAL, "dpow_board_counters: NULL argument");
     Lock lk(&b->mem->h.lock);
+    if (!lk.held()) return lock_lost("dpow_board_counters");
     *tasks = b->mem->h.tasks;
     *shared_gpu = __atomic_load_n(&b->mem->h.shared, __ATOMIC_RELAXED);
     return 0;
@@ -220,6 +252,7 @@ int dpow_board_counters(dpow_board *b, uint64_t *tasks, uint64_t *shared_gpu) {
 int dpow_board_tasks(dpow_board *b) {
     if (!b || !b->mem) return dpow::fail(DPOW_EINVAL, "dpow_board_tasks: board is NULL");
     Lock lk(&b->mem->h.lock);
+    if (!lk.held()) return lock_lost("dpow_board_tasks");
     int n = 0;
     for (uint32_t i = 0; i < kEntries; ++i) n += b->mem->e[i].state == 1 ? 1 : 0;
     return n;
@@ -285,6 +318,7 @@ int board_join(dpow_board *b, const uint8_t *nonce, size_t nonce_len, uint32_t n
     Layout &L = *b->mem;
     const uint64_t bit = 1ull << rank;
     Lock lk(&L.h.lock);
+    if (!lk.held()) return lock_lost("dpow_board_join");
     // The task's entry: the active one with this key that rank has not joined yet (an entry the
     // rank already joined belongs to an earlier task with the same key whose other ranks are
     // still leaving it).
@@ -325,8 +359,7 @@ int board_join(dpow_board *b, const uint8_t *nonce, size_t nonce_len, uint32_t n
 // GPU is seen, "yes" needs the full set of W keys, which all ranks then read alike.
 int same_gpu(const Entry &e, uint32_t world, uint64_t mine, const volatile uint32_t *cancel) {
     const uint64_t full = world == 64 ? ~0ull : (1ull << world) - 1;
-    const int64_t t0 = std::chrono::duration_cast<std::chrono::nanoseconds>(
-                           std::chrono::steady_clock::now().time_since_epoch()).count();
+    const int64_t t0 = mono_ns();
     for (uint64_t it = 0;; ++it) {
         const uint64_t m = __atomic_load_n(&e.joined, __ATOMIC_ACQUIRE);
         for (uint32_t r = 0; r < world; ++r)
@@ -337,8 +370,7 @@ int same_gpu(const Entry &e, uint32_t world, uint64_t mine, const volatile uint3
             __builtin_ia32_pause();
             continue;
         }
-        const int64_t t = std::chrono::duration_cast<std::chrono::nanoseconds>(
-                              std::chrono::steady_clock::now().time_since_epoch()).count();
+        const int64_t t = mono_ns();
         if (t - t0 > kVoteTimeoutNs)
             return dpow::fail(DPOW_EPROTO, "dpow_board_search: the task's other ranks never joined the board");
         const struct timespec d = {0, 2000};

@@ -156,3 +156,29 @@ def test_two_processes_share_a_named_board():
     with Board(name) as b:  # re-created empty after the unlink
         assert b.tasks() == 0
     distpow.lib().dpow_board_unlink(name.encode())
+
+
+def test_a_lock_held_by_a_dead_process_is_an_error_not_a_hang():
+    """The board's spin lock is held for a few hundred ns by a join or leave; one held for 10 s
+    belongs to a process that died inside: the caller gets DPOW_EPROTO instead of spinning."""
+    import mmap
+    import time
+    name = f"/dpow_test_lock_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    try:
+        with Board(name) as b:
+            fd = os.open("/dev/shm" + name, os.O_RDWR)
+            try:
+                m = mmap.mmap(fd, 4096)
+            finally:
+                os.close(fd)
+            m[8:12] = (1).to_bytes(4, "little")  # Header::lock, taken by "a dead process"
+            t0 = time.time()
+            with pytest.raises(distpow.DpowError) as e:
+                b.join(N1, 7, 2, 0)
+            assert e.value.code == EPROTO and "lock" in str(e.value)
+            assert 9 < time.time() - t0 < 30
+            m[8:12] = bytes(4)
+            m.close()
+            b.join(N1, 7, 2, 0)  # released: usable again
+    finally:
+        distpow.lib().dpow_board_unlink(name.encode())

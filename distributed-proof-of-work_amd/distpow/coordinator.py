@@ -51,17 +51,26 @@ def _bytes_greater(a: bytes, b: bytes) -> bool:  # bytes.Compare(a, b) > 0
 
 class Coordinator:
     def __init__(self, n_workers: int, devices: Sequence[int] = (0,), timeout_s: float = 600.0,
-                 node: Optional[bool] = None):
+                 node: Optional[bool] = None, workers: Optional[Sequence] = None):
+        """workers: the W workers to drive instead of in-process ones -- anything with the Worker
+        methods, e.g. distpow.procworker.ProcessWorker (one worker process each, which opens the
+        node's named board itself); the coordinator then owns their lifetime but no board."""
+        if workers is not None:
+            n_workers = len(workers)
         if n_workers < 1:
             raise ValueError("need at least one worker")
         pow2 = 2 <= n_workers <= 64 and n_workers & (n_workers - 1) == 0
         if node and not pow2:
             raise ValueError("node mode needs W a power of two in [2, 64] (coordinator.go:326 partitions)")
-        self.workers: List[Worker] = [Worker(devices[i % len(devices)]) for i in range(n_workers)]
-        self.board: Optional[Board] = Board() if (pow2 if node is None else node) else None
-        if self.board is not None:
-            for w in self.workers:
-                w.set_board(self.board)
+        self.board: Optional[Board] = None
+        if workers is not None:
+            self.workers = list(workers)
+        else:
+            self.workers: List[Worker] = [Worker(devices[i % len(devices)]) for i in range(n_workers)]
+            self.board = Board() if (pow2 if node is None else node) else None
+            if self.board is not None:
+                for w in self.workers:
+                    w.set_board(self.board)
         self.worker_bytes = [i & 0xFF for i in range(n_workers)]  # workerByte = uint8(i), coordinator.go:127
         self.worker_bits = int(math.log2(n_workers))              # uint(math.Log2(float64(W))), coordinator.go:326
         self.timeout_s = timeout_s

@@ -176,3 +176,42 @@ def test_non_power_of_two_workers_quirk():
         assert c.worker_bits == 1 and c.board is None
         s = c.mine([9, 9, 9, 9], 4)
         assert ok([9, 9, 9, 9], s, 4)
+
+
+@pytest.mark.parametrize("split", [False, True], ids=["one_gpu", "per_rank"])
+def test_worker_processes_share_a_named_board(golden, split):
+    """The reference's topology: one worker process per GPU (here 4 processes on GPU 0), each
+    opening the node's board by name (DPOW_NODE_BOARD in INTEGRATION.md), driven by the unchanged
+    coordinator protocol over pipes (distpow.procworker).  Config 3's answer is the golden, sent
+    by its owner's process only; the board holds no task afterwards."""
+    import os
+    import uuid
+
+    from distpow.procworker import ProcessWorker
+    from distpow.worker import Board
+    name = f"/dpow_test_proc_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    env = {"DPOW_DIAG_BOARD_SPLIT": "1"} if split else {}
+    want, g = golden_secret(golden, N1, 7)
+    owner = (g & 255) >> 6
+    try:
+        with Board(name) as board:  # the parent's view of the same board (counters)
+            workers = [ProcessWorker(0, name, env) for _ in range(4)]
+            with Coordinator(4, workers=workers) as c:
+                assert c.board is None and c.worker_bits == 2
+                assert c.mine(N1, 7, token=401) == want
+                res = [t for t in c.trace() if t["trace"] == 401 and t["action"] == "CoordinatorWorkerResult"]
+                assert [(t["WorkerByte"], bytes(t["Secret"])) for t in res] == [(owner, want)]
+                for w, wb in zip(c.workers, c.worker_bytes):
+                    seq = [t["action"] for t in w.trace() if t["trace"] == 401 and
+                           t["action"] in ("WorkerMine", "WorkerResult", "WorkerCancel")]
+                    assert seq == (["WorkerMine", "WorkerResult", "WorkerCancel"] if wb == owner
+                                   else ["WorkerMine", "WorkerCancel"]), (wb, seq)
+                want8, _ = golden_secret(golden, [2, 2, 2, 2], 8)
+                assert c.mine([2, 2, 2, 2], 8) == want8
+                assert not [t for t in c.trace() if t["action"] == "CoordinatorDroppedResult"]
+            assert board.tasks() == 0
+            tasks, shared = board.counters()
+            assert tasks == 2 and shared == (0 if split else 2), (tasks, shared)
+    finally:
+        import distpow
+        distpow.lib().dpow_board_unlink(name.encode())

@@ -174,3 +174,23 @@ def test_coordinator_fails_fast_on_worker_error():
             c.mine(N1, 5)
         assert time.perf_counter() - t0 < 10
         assert "CoordinatorWorkerError" in [t["action"] for t in c.trace()]
+
+
+def test_process_workers_drive_like_in_process_ones():
+    """distpow.procworker: the coordinator drives W worker processes over pipes exactly as it
+    drives in-process workers -- Mine, the ResultChannel, the trace -- and, with no GPU visible
+    here, fails the request at once on their error messages (no hang)."""
+    from distpow.coordinator import Coordinator, CoordinatorProtocolError
+    from distpow.procworker import ProcessWorker
+    if distpow.device_count() > 0:
+        pytest.skip("needs a host without a visible GPU")
+    workers = [ProcessWorker(0) for _ in range(2)]
+    with Coordinator(2, workers=workers, timeout_s=600) as c:
+        assert c.board is None and c.worker_bits == 1
+        t0 = time.perf_counter()
+        with pytest.raises(CoordinatorProtocolError, match="search failed"):
+            c.mine(N1, 5, token=9)
+        assert time.perf_counter() - t0 < 30
+        acts = [t["action"] for t in workers[0].trace() if t["trace"] == 9]
+        assert acts[:2] == ["WorkerMine", "CacheMiss"] and "MinerError" in acts
+    assert all(not w._proc.is_alive() for w in workers)

@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -102,23 +103,32 @@ struct dpow_worker {
     std::vector<std::string> trace;
     std::mutex pool_mu;                                     // one dpow_ctx per concurrent search
     std::vector<dpow_ctx *> pool;
-    struct Runner {  // one miner goroutine (worker.go:182)
-        std::thread th;
-        std::shared_ptr<Task> task;
-        std::shared_ptr<std::atomic<bool>> done;
-    };
+    // The miner goroutines (worker.go:182): a pool of threads, each running one task's miner at
+    // a time.  A Mine hands its task to an idle pool thread (a condition-variable wake) or starts
+    // a new one: creating a thread per Mine cost ~20 us of the Mine call, which a node's ranks
+    // wait out before their search starts (dpow_board_search waits for all W ranks to join).
     std::mutex thr_mu;
-    std::vector<Runner> runners;
+    std::condition_variable thr_cv;
+    std::deque<std::shared_ptr<Task>> pending;      // handed over, not yet picked up
+    std::vector<std::shared_ptr<Task>> running;     // picked up by a pool thread, miner not returned
+    std::vector<std::thread> threads;
+    size_t idle = 0;
+    bool closing = false;
 
-    void reap_locked() {  // join miners that returned
-        for (size_t i = 0; i < runners.size();) {
-            if (runners[i].done->load()) {
-                runners[i].th.join();
-                runners[i] = std::move(runners.back());
-                runners.pop_back();
-            } else {
-                ++i;
-            }
+    void pool_thread() {
+        std::unique_lock<std::mutex> g(thr_mu);
+        for (;;) {
+            ++idle;
+            thr_cv.wait(g, [&] { return closing || !pending.empty(); });
+            --idle;
+            if (pending.empty()) return;  // closing, nothing left
+            std::shared_ptr<Task> t = pending.front();
+            pending.pop_front();
+            running.push_back(t);  // with the pop, under one lock: a closing worker kills it
+            g.unlock();
+            miner(t);
+            g.lock();
+            running.erase(std::find(running.begin(), running.end(), t));
         }
     }
 
@@ -333,11 +343,14 @@ int dpow_worker_new(int device, dpow_worker **out) {
 void dpow_worker_free(dpow_worker *w) {
     if (!w) return;
     {
+        // every miner, running or still pending, ends at its next kill wait (a pending one at once)
         std::lock_guard<std::mutex> g(w->thr_mu);
-        for (auto &r : w->runners) dpow_worker::kill(*r.task);  // every running miner ends at its next kill wait
+        w->closing = true;
+        for (auto &t : w->running) dpow_worker::kill(*t);
+        for (auto &t : w->pending) dpow_worker::kill(*t);
+        w->thr_cv.notify_all();
     }
-    for (auto &r : w->runners)
-        if (r.th.joinable()) r.th.join();
+    for (auto &th : w->threads) th.join();
     for (dpow_ctx *c : w->pool) dpow_close(c);
     delete w;
 }
@@ -364,16 +377,9 @@ int dpow_worker_mine(dpow_worker *w, const uint8_t *nonce, size_t nonce_len, uin
     const uint32_t wb = worker_byte;
     w->record(token, "WorkerMine", dpow_worker::fields(t->nonce, ntz, nullptr, &wb));
     std::lock_guard<std::mutex> g(w->thr_mu);
-    w->reap_locked();
-    auto done = std::make_shared<std::atomic<bool>>(false);
-    dpow_worker::Runner r;
-    r.task = t;
-    r.done = done;
-    r.th = std::thread([w, t, done] {  // go miner(...)
-        w->miner(t);
-        done->store(true);
-    });
-    w->runners.push_back(std::move(r));
+    w->pending.push_back(t);  // go miner(...)
+    if (w->idle >= w->pending.size()) w->thr_cv.notify_one();
+    else w->threads.emplace_back([w] { w->pool_thread(); });
     return 0;
 }
 

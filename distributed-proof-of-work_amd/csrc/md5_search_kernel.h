@@ -150,7 +150,57 @@ DPOW_DEV_CONST bool seg_word(int m) {
 // per-layout sweep of builds with one start for every layout
 // (one start for every layout, 1..6: tools/lead_sweep.py, profiles/r02_lead_sweep.json),
 // where a start beats 4 by >= 0.8 %.  The headline <1,1,0> keeps 4.
-constexpr int pipe_lead(int nblk, int w0, int sh) {
+// The build choices of the narrow SH = 3 kernels (hash_wave_block KSPAN = false, the kernels of
+// launches with R >= 64): pipe start (0: the general kernel's), VGPR-constant cap (0: the
+// general's), kLaunchPoll (-1: the general's) and SGPR budget class (-1: the general's; 1 = 96,
+// 2 = 100).  Each row is the per-layout argmax of round 6's same-box sweeps of builds with one
+// choice for every narrow kernel (tools/lead_sweep.py; profiles/r06_narrow_sweep.json).  on =
+// false: no narrow build beat the layout's general kernel (<1,0,3>), or the layout was not swept
+// (<1,12..13,3>: chunks below 2^24 only), so it runs the general kernel for every R.
+struct NarrowKnobs {
+    bool on;
+    int lead, cap, poll, sgpr;
+};
+constexpr NarrowKnobs narrow_knobs(int nblk, int w0) {
+    if (nblk == 1) {
+        switch (w0) {
+            case 1: case 2: case 3: case 5: case 6: case 11:
+                    return {true, 2, 0, 0, 1};
+            case 4: return {true, 1, 0, -1, -1};
+            case 7: return {true, 2, 0, -1, 1};
+            case 8: return {true, 3, 0, 0, -1};
+            case 9: return {true, 4, 0, -1, -1};
+            case 10: return {true, 2, 0, 0, -1};
+            default: return {false, 0, 0, -1, -1};
+        }
+    }
+    switch (w0) {
+        case 12: return {true, 3, 0, 0, -1};
+        case 13: return {true, 3, 0, -1, -1};
+        case 14: return {true, 2, 24, -1, -1};
+        case 15: return {true, 2, 0, 0, -1};
+        default: return {false, 0, 0, -1, -1};
+    }
+}
+// A/B builds only: one choice for every narrow kernel, over the table (tools/lead_sweep.py)
+#ifndef DPOW_NLEAD
+#define DPOW_NLEAD 0   // pipe start
+#endif
+#ifndef DPOW_NCAP
+#define DPOW_NCAP 0    // VGPR-constant cap
+#endif
+#ifndef DPOW_NPOLL
+#define DPOW_NPOLL -1  // kLaunchPoll 0 / 1
+#endif
+#ifndef DPOW_NSGPR
+#define DPOW_NSGPR 0   // SGPR budget class 1 / 2
+#endif
+
+constexpr int pipe_lead(int nblk, int w0, int sh, bool narrow = false) {
+    if (narrow) {
+        const int lead = DPOW_NLEAD > 0 ? DPOW_NLEAD : narrow_knobs(nblk, w0).lead;
+        if (lead > 0) return lead;
+    }
     // (round 4: the same sweep over the round-4 kernels, profiles/r04_lead_sweep.json, moved the
     // entries marked r4 -- a start that beats the table's by >= 1 % -- and dropped <1,10,1..2>'s
     // 3, now 7.4 % below 4)
@@ -190,12 +240,14 @@ constexpr int pipe_lead(int nblk, int w0, int sh) {
     }
 }
 
-template <int NBLK, int W0, int SH>
+// KS: the KSPAN argument of the kernel (hash_wave_block); kNarrow = SH = 3's narrow kernel.
+template <int NBLK, int W0, int SH, bool KS = true>
 struct VgprK {
+    static constexpr bool kNarrow = SH == 3 && !KS;
     // First step of block 0 in the hand-ordered pipeline (md5_tail's kI0 for
     // the hash loop's ONLY_D call with kNC candidates).
     static constexpr int kEnd0 = NBLK == 1 ? 62 : 64;
-    static constexpr int kLead = pipe_lead(NBLK, W0, SH);
+    static constexpr int kLead = pipe_lead(NBLK, W0, SH, kNarrow);
     static constexpr int kI0 = W0 + kLead < kEnd0 ? W0 + kLead : kEnd0;
     // Steps the hash loop runs (ONLY_D: the last block stops after step 61).
     static constexpr bool run(int blk, int i) { return !(blk == NBLK - 1 && i >= 62); }
@@ -235,7 +287,9 @@ struct VgprK {
     // (round 4, profiles/r04_lead_sweep.json: a cap of 24 for <1,7,1..2> +1.9-2.0 %,
     // <1,4,3> +1.5 %, <1,5,3> +1.0 %; elsewhere it is no better, or costs up to 3 %)
     static constexpr bool kCap24 = NBLK == 1 && ((W0 == 7 && (SH == 1 || SH == 2)) || (SH == 3 && (W0 == 4 || W0 == 5)));
-    static constexpr int kCap = kCap24 ? 24
+    static constexpr int kNarrowCap = DPOW_NCAP > 0 ? DPOW_NCAP : narrow_knobs(NBLK, W0).cap;
+    static constexpr int kCap = kNarrow && kNarrowCap > 0 ? kNarrowCap
+                                : kCap24 ? 24
                                 : NBLK == 1 ? (SH == 0 ? 24 : SH == 3 ? 14 : 18)
                                             : (SH == 3 ? 20 : 26);
     static constexpr bool use(int blk, int i) {
@@ -243,13 +297,13 @@ struct VgprK {
     }
 };
 
-template <int NBLK, int W0, int SH, int BLK, int I>
+template <int NBLK, int W0, int SH, int BLK, int I, bool KS>
 DPOW_DEV void kconst_init(KConst &kc, const Launch &L) {
     if constexpr (BLK < NBLK) {
-        if constexpr (VgprK<NBLK, W0, SH>::use(BLK, I))
+        if constexpr (VgprK<NBLK, W0, SH, KS>::use(BLK, I))
             asm("v_mov_b32 %0, %1" : "=v"(kc.v[64 * BLK + I]) : "s"(L.KT[64 * BLK + I]));
-        if constexpr (I + 1 < 64) kconst_init<NBLK, W0, SH, BLK, I + 1>(kc, L);
-        else kconst_init<NBLK, W0, SH, BLK + 1, 0>(kc, L);
+        if constexpr (I + 1 < 64) kconst_init<NBLK, W0, SH, BLK, I + 1, KS>(kc, L);
+        else kconst_init<NBLK, W0, SH, BLK + 1, 0, KS>(kc, L);
     }
 }
 
@@ -290,27 +344,31 @@ DPOW_DEV void seg_all_deltas(const Launch &L, uint32_t sg, uint32_t &d0, uint32_
 
 // Re-derive the VGPR-held K + M constants of the segment words (wave-uniform,
 // once per segment change: a rare branch).
-template <int NBLK, int W0, int SH, int BLK, int I>
+template <int NBLK, int W0, int SH, int BLK, int I, bool KS>
 DPOW_DEV void kconst_seg(KConst &kc, const Launch &L, const uint32_t (&d)[3]) {
     if constexpr (BLK < NBLK) {
-        if constexpr (VgprK<NBLK, W0, SH>::seg(BLK, I)) {
+        if constexpr (VgprK<NBLK, W0, SH, KS>::seg(BLK, I)) {
             constexpr int m = 16 * BLK + md5_word(I);
             const uint32_t k = L.KT[64 * BLK + I] + seg_add<NBLK, W0>(m, d);
             asm volatile("v_mov_b32 %0, %1" : "=v"(kc.v[64 * BLK + I]) : "s"(k));
         }
-        if constexpr (I + 1 < 64) kconst_seg<NBLK, W0, SH, BLK, I + 1>(kc, L, d);
-        else kconst_seg<NBLK, W0, SH, BLK + 1, 0>(kc, L, d);
+        if constexpr (I + 1 < 64) kconst_seg<NBLK, W0, SH, BLK, I + 1, KS>(kc, L, d);
+        else kconst_seg<NBLK, W0, SH, BLK + 1, 0, KS>(kc, L, d);
     }
 }
 
-// Per-candidate variable message parts.
+// Per-candidate variable message parts.  KSPAN: the lanes may span several k (R < 64), so
+// SH = 3's word W0 + 1 differs per lane (lane_k); without it that word's K + M is wave-uniform.
+template <bool KSPAN>
 struct VarWords {
+    static constexpr bool kSpan = KSPAN;
     uint32_t lo_s[kNC];  // wave-uniform part of V << 8*SH (word W0)
     uint32_t lo_v;       // per-lane part of V << 8*SH (the same for every slot)
     uint32_t hi_s[kNC];  // SH != 0: the wave-uniform part of word W0+1's addition -- V >> (32 - 8 SH)
                          //  (uniform: a lane's k offset never carries into those bits) plus the
                          //  segment addition d1
-    uint32_t lane_k;     // SH = 3: the per-lane part of V >> 8 (the lane's k offset; 0 when R >= 64)
+    uint32_t lane_k;     // SH = 3: the per-lane part of V >> 8 (the lane's k offset; 0 when R >= 64,
+                         //  and not read without KSPAN)
     const KConst *kc;    // launch-uniform K + M constants held in VGPRs (segment words: current segment)
     uint32_t seg_d[3];   // segment-word additions (seg_add) for the steps that read them from L.KT
                          //  (full_check's steps 62-63 of the last block only; the hash loop holds them
@@ -319,37 +377,37 @@ struct VarWords {
 
 // K + M of step I of block BLK for candidate j (the message word M includes the
 // candidate's variable bytes when the step reads word W0, or W0 + 1 for SH != 0).
-template <int NBLK, int W0, int SH, int BLK, int I>
+template <int NBLK, int W0, int SH, int BLK, int I, bool KS>
 struct StepWord {
     static constexpr int m = 16 * BLK + md5_word(I);
     // Words past the variable bytes, the chunk tail and the 0x80 pad -- every
     // word after W0 + 2 except the bit-length word -- are zero for every launch
     // of this layout (plan.cpp), so K + M folds to the literal K: no SGPR.
     static constexpr bool zero_word = m > W0 + 2 && m != 16 * NBLK - 2;
-    static constexpr bool per_lane = m == W0 || (SH == 3 && m == W0 + 1);  // K + M differs per lane
-    static constexpr bool vgpr_k = VgprK<NBLK, W0, SH>::use(BLK, I);
+    static constexpr bool per_lane = m == W0 || (SH == 3 && KS && m == W0 + 1);  // K + M differs per lane
+    static constexpr bool vgpr_k = VgprK<NBLK, W0, SH, KS>::use(BLK, I);
     static constexpr bool seg = seg_word<NBLK, W0, SH>(m);
-    static DPOW_DEV uint32_t km(const Launch &L, const VarWords &v, int j) {
+    static DPOW_DEV uint32_t km(const Launch &L, const VarWords<KS> &v, int j) {
         uint32_t k = zero_word ? kMd5K[I] : vgpr_k ? v.kc->v[64 * BLK + I] : L.KT[64 * BLK + I];
         if constexpr (seg && !vgpr_k) k += seg_add<NBLK, W0>(m, v.seg_d);
         if constexpr (m == W0) k = (k + v.lo_s[j]) + v.lo_v;
         if constexpr (SH != 0 && m == W0 + 1) {
             k += v.hi_s[j];                        // SALU: K + M stays uniform
-            if constexpr (SH == 3) k += v.lane_k;  // the one VALU add of the step
+            if constexpr (SH == 3 && KS) k += v.lane_k;  // the one VALU add of the step
         }
         return k;
     }
 };
 
 // Steps [I, IE) of block BLK for NCAND candidates, left to the compiler.
-template <int NBLK, int W0, int SH, int BLK, int I, int IE, int NCAND>
-DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
+template <int NBLK, int W0, int SH, int BLK, int I, int IE, int NCAND, class V>
+DPOW_DEV void md5_steps(uint32_t (&x)[4][kNC], const Launch &L, const V &v) {
     if constexpr (I < IE) {
         constexpr int ai = (64 - I) % 4, bi = (ai + 1) % 4, ci = (ai + 2) % 4, di = (ai + 3) % 4;
         constexpr int s = md5_shift(I);
 #pragma unroll
         for (int j = 0; j < NCAND; ++j) {
-            const uint32_t km = StepWord<NBLK, W0, SH, BLK, I>::km(L, v, j);
+            const uint32_t km = StepWord<NBLK, W0, SH, BLK, I, V::kSpan>::km(L, v, j);
             const uint32_t f = md5_fn<I>(x[bi][j], x[ci][j], x[di][j]);
             x[ai][j] = x[bi][j] + __builtin_rotateleft32(x[ai][j] + f + km, s);
         }
@@ -427,10 +485,10 @@ template <int I> struct Roles {
 // plain `+v` lets the register allocator hand q's input that same register, which
 // the group then overwrites before q reads it (a wrong hash in <1,0,0> at start
 // W0 + 2, caught by test_nonce_lengths_golden / tools/layout_check.py).
-template <int NBLK, int W0, int SH, int BLK, int I, int J>
-DPOW_DEV void body(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const VarWords &v) {
+template <int NBLK, int W0, int SH, int BLK, int I, int J, class V>
+DPOW_DEV void body(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const V &v) {
     using R = Roles<I>;  // q's step I-1 writes x[R::b][q] from x[R::c][q]
-    using W = StepWord<NBLK, W0, SH, BLK, I>;
+    using W = StepWord<NBLK, W0, SH, BLK, I, V::kSpan>;
     const uint32_t kp = W::km(L, v, J), kq = W::km(L, v, J + 1);
     uint32_t fp, fq, rq, tp;
     if constexpr (W::per_lane || W::vgpr_k)
@@ -450,10 +508,10 @@ DPOW_DEV void body(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const V
 }
 
 // Prologue of a pair at its first pipelined step I0: q's step I0 is left half done.
-template <int NBLK, int W0, int SH, int BLK, int I0, int J>
-DPOW_DEV void prologue(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const VarWords &v) {
+template <int NBLK, int W0, int SH, int BLK, int I0, int J, class V>
+DPOW_DEV void prologue(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, const V &v) {
     using R = Roles<I0>;
-    using W = StepWord<NBLK, W0, SH, BLK, I0>;
+    using W = StepWord<NBLK, W0, SH, BLK, I0, V::kSpan>;
     const uint32_t kp = W::km(L, v, J), kq = W::km(L, v, J + 1);
     uint32_t fp, fq, tp;
     if constexpr (W::per_lane || W::vgpr_k)
@@ -473,8 +531,8 @@ DPOW_DEV void prologue(uint32_t (&x)[4][kNC], uint32_t &tq, const Launch &L, con
 constexpr int kPairs = kNC / 2;
 
 // Step pairs I .. IE-1 of every candidate pair, the pairs' groups interleaved.
-template <int NBLK, int W0, int SH, int BLK, int I, int IE>
-DPOW_DEV void run(uint32_t (&x)[4][kNC], uint32_t (&tq)[kPairs], const Launch &L, const VarWords &v) {
+template <int NBLK, int W0, int SH, int BLK, int I, int IE, class V>
+DPOW_DEV void run(uint32_t (&x)[4][kNC], uint32_t (&tq)[kPairs], const Launch &L, const V &v) {
     if constexpr (I < IE) {
         body<NBLK, W0, SH, BLK, I, 0>(x, tq[0], L, v);
         if constexpr (kPairs > 1) body<NBLK, W0, SH, BLK, I, 2>(x, tq[1], L, v);
@@ -483,8 +541,8 @@ DPOW_DEV void run(uint32_t (&x)[4][kNC], uint32_t (&tq)[kPairs], const Launch &L
 }
 
 // Steps [I0, IE) of block BLK for all candidates in the alternating order.
-template <int NBLK, int W0, int SH, int BLK, int I0, int IE>
-DPOW_DEV void steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
+template <int NBLK, int W0, int SH, int BLK, int I0, int IE, class V>
+DPOW_DEV void steps(uint32_t (&x)[4][kNC], const Launch &L, const V &v) {
     static_assert(kNC == 2 || kNC == 4, "the pipelined path runs one or two candidate pairs");
     if constexpr (I0 < IE) {
         uint32_t tq[kPairs];
@@ -511,8 +569,8 @@ DPOW_DEV void steps(uint32_t (&x)[4][kNC], const Launch &L, const VarWords &v) {
 // only feed A..C): out[3] is exact, out[0..2] are not computed.  With RAW_D
 // (one final block) out[3] is the state word without the chaining value:
 // D = iv[3] + out[3], which the D-equality test compares against -iv[3].
-template <int NBLK, int W0, int SH, int NCAND, bool ONLY_D = false, bool RAW_D = false>
-DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords &v) {
+template <int NBLK, int W0, int SH, int NCAND, bool ONLY_D = false, bool RAW_D = false, class V>
+DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const V &v) {
     static_assert(!RAW_D || (ONLY_D && NBLK == 1), "RAW_D: D word of one final block");
     uint32_t x[4][kNC];
 #pragma unroll
@@ -524,7 +582,7 @@ DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords 
     // wave-uniform or partly so, and the compiler folds them).
     constexpr bool kPipe = NCAND == kNC && (kNC == 2 || kNC == 4);
     constexpr int kEnd0 = (ONLY_D && NBLK == 1) ? 62 : 64;
-    constexpr int kLead = pipe_lead(NBLK, W0, SH);
+    constexpr int kLead = VgprK<NBLK, W0, SH, V::kSpan>::kLead;
     constexpr int kI0 = kPipe ? (W0 + kLead < kEnd0 ? W0 + kLead : kEnd0) : kEnd0;
     md5_steps<NBLK, W0, SH, 0, 0, kI0, NCAND>(x, L, v);
     if constexpr (kPipe) pipe::steps<NBLK, W0, SH, 0, kI0, kEnd0>(x, L, v);
@@ -554,13 +612,13 @@ DPOW_DEV void md5_tail(uint32_t (&out)[4][kNC], const Launch &L, const VarWords 
 // (i0 is a multiple of 64), so the sum never carries and V's bits above the
 // lane's k offset are wave-uniform: V >> 24 and V >> 16 are uniform, and
 // V >> 8 = (vs >> 8) + (loff >> 8).  d1 = the segment addition to word W0 + 1.
-template <int SH>
-DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff, uint32_t d1) {
+template <int SH, class V>
+DPOW_DEV void var_words(V &v, int j, uint32_t vs, uint32_t loff, uint32_t d1) {
     v.lo_s[j] = vs << (8 * SH);
     v.lo_v = loff << (8 * SH);
     if constexpr (SH != 0) {
         v.hi_s[j] = (vs >> (32 - 8 * SH)) + d1;
-        v.lane_k = SH == 3 ? loff >> 8 : 0u;
+        v.lane_k = SH == 3 && V::kSpan ? loff >> 8 : 0u;
     } else {
         v.hi_s[j] = 0u;
         v.lane_k = 0u;
@@ -573,9 +631,10 @@ DPOW_DEV void var_words(VarWords &v, int j, uint32_t vs, uint32_t loff, uint32_t
 // sd: the segment's word additions (seg_all_deltas), computed by the caller outside the
 // per-lane branch (a dynamic kernarg index inside it moved the hash loop's wave-uniform
 // index arithmetic onto the VALU: +10 VALU per wave-block in <1,1,0>, tools/isa_loop.py).
-template <int NBLK, int W0, int SH>
+// KS: the kernel's KSPAN (kc holds the constants VgprK<.., KS> selects).
+template <int NBLK, int W0, int SH, bool KS>
 DPOW_DEV bool full_check(const Launch &L, const KConst &kc, uint32_t vs, uint32_t loff, const uint32_t (&sd)[3]) {
-    VarWords v;
+    VarWords<KS> v;
     v.kc = &kc;
     v.seg_d[0] = sd[0];
     v.seg_d[1] = sd[1];
@@ -772,11 +831,16 @@ DPOW_DEV uint64_t lane_range_mask(int64_t lo, int64_t hi) {
 // in the wave, 16^-(ntz & ~1) per candidate) re-tests against the exact mask.
 constexpr uint64_t kNoHitG = ~0ull;
 
-template <int NBLK, int W0, int SH, bool EQ>
+// KSPAN (SH = 3 only): the launch's lanes may span several k (R < 64), so word W0 + 1's
+// K + M carries each lane's k offset (VarWords::lane_k, one VALU add per candidate in each
+// of that word's four steps).  The SH = 3 kernels of launches with R >= 64 (workerBits <= 2:
+// the offset is 0) are instantiated without it: the word's K + M stays a wave-uniform SGPR.
+template <int NBLK, int W0, int SH, bool EQ, bool KSPAN>
 DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0, uint32_t lane, uint32_t loff) {
     static_assert(!EQ || NBLK == 1, "the D-equality test needs one final block");
+    static_assert(KSPAN || SH == 3, "only the SH = 3 kernels have a narrow (R >= 64) instantiation");
     uint32_t vs[kNC];
-    VarWords v;
+    VarWords<KSPAN> v;
     v.kc = &kc;
     v.seg_d[0] = v.seg_d[1] = v.seg_d[2] = 0u;  // unused: the hash loop's segment-word steps all read kc
     uint32_t d1 = 0u;               // SH != 0: the segment addition to word W0 + 1 (both slots share
@@ -808,7 +872,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
             if (m != 0 && L.ntz > 8u) {
                 uint32_t d0, sd[3];
                 seg_all_deltas<NBLK, W0, SH>(L, seg_id((ij < L.i_begin ? L.i_begin : ij) >> L.rbits), d0, sd);
-                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH>(L, kc, vs[j], loff, sd);
+                const bool ok = ((m >> lane) & 1ull) && full_check<NBLK, W0, SH, KSPAN>(L, kc, vs[j], loff, sd);
                 m = __ballot(ok);
             }
             if (m != 0) {
@@ -860,7 +924,20 @@ constexpr bool kW15Sgpr = (NBLK == 2 && W0 == 15) || (NBLK == 2 && SH == 3 && (W
 template <int NBLK, int W0, int SH>
 constexpr bool kLaunchPoll = NBLK == 1 || SH == 1 || SH == 2 || (SH == 0 && W0 == 15) || (SH == 3 && W0 >= 14);
 
-template <int NBLK, int W0, int SH, bool EQ>
+// The choices of a kernel (KS: its KSPAN; the narrow SH = 3 kernels' from narrow_knobs):
+// kLaunchPoll and the SGPR budget class (0: DPOW_NUM_SGPR, 1: _LONG, 2: _W15).
+template <int NBLK, int W0>
+constexpr int kNarrowPoll = DPOW_NPOLL >= 0 ? DPOW_NPOLL : narrow_knobs(NBLK, W0).poll;
+template <int NBLK, int W0>
+constexpr int kNarrowSgpr = DPOW_NSGPR > 0 ? DPOW_NSGPR : narrow_knobs(NBLK, W0).sgpr;
+template <int NBLK, int W0, int SH, bool KS>
+constexpr bool kPollOf = SH == 3 && !KS && kNarrowPoll<NBLK, W0> >= 0 ? kNarrowPoll<NBLK, W0> != 0
+                                                                     : kLaunchPoll<NBLK, W0, SH>;
+template <int NBLK, int W0, int SH, bool KS>
+constexpr int kSgprOf = SH == 3 && !KS && kNarrowSgpr<NBLK, W0> > 0 ? kNarrowSgpr<NBLK, W0>
+                        : kW15Sgpr<NBLK, W0, SH> ? 2 : kLongSgpr<NBLK, W0> ? 1 : 0;
+
+template <int NBLK, int W0, int SH, bool EQ, bool KSPAN>
 DPOW_DEV void search_body(const Launch &L) {
     if (blockIdx.x == 0) {  // dispatched first: the watcher
         watcher(L);
@@ -882,7 +959,7 @@ DPOW_DEV void search_body(const Launch &L) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t loff = lane_offset(L.rbits, lane);
     KConst kc;
-    kconst_init<NBLK, W0, SH, 0, 0>(kc, L);
+    kconst_init<NBLK, W0, SH, 0, 0, KSPAN>(kc, L);
     // The 2^24-k segment kc's segment-word constants belong to; kept in a VGPR
     // (wave-uniform, read once per group): an SGPR live across the hash loop
     // costs spill reloads inside it under the 80-SGPR budget.
@@ -997,7 +1074,7 @@ DPOW_DEV void search_body(const Launch &L) {
         uint64_t i0 = i_first;
         uint32_t left = nb;
         // (some two-block layouts: the compile-time group, kLaunchPoll)
-        const uint32_t poll_wb = kLaunchPoll<NBLK, W0, SH> ? L.poll_wb : (uint32_t)DPOW_POLL_WB;
+        const uint32_t poll_wb = kPollOf<NBLK, W0, SH, KSPAN> ? L.poll_wb : (uint32_t)DPOW_POLL_WB;
         for (;;) {
             uint32_t q = left < poll_wb ? left : poll_wb;
             // A chunk never straddles a 2^24-k segment boundary (the host aligns a
@@ -1013,7 +1090,7 @@ DPOW_DEV void search_body(const Launch &L) {
                     asm volatile("v_mov_b32 %0, %1" : "=v"(cur_seg_v) : "s"(sg));
                     uint32_t d0, d[3];
                     seg_all_deltas<NBLK, W0, SH>(L, sg, d0, d);
-                    kconst_seg<NBLK, W0, SH, 0, 0>(kc, L, d);
+                    kconst_seg<NBLK, W0, SH, 0, 0, KSPAN>(kc, L, d);
                     if constexpr (SH == 0) lov = lane_offset(L.rbits, lane) + d0;
                 }
             }
@@ -1032,7 +1109,7 @@ DPOW_DEV void search_body(const Launch &L) {
 #if DPOW_WAVE_TRACE
                 ++n_wb;
 #endif
-                const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ>(L, kc, i0, lane, SH == 0 ? lov : loff);
+                const uint64_t g = hash_wave_block<NBLK, W0, SH, EQ, KSPAN>(L, kc, i0, lane, SH == 0 ? lov : loff);
                 if (g != kNoHitG) {
                     best = g < best ? g : best;
                     hit = true;
@@ -1121,7 +1198,7 @@ DPOW_DEV void search_body(const Launch &L) {
                 }
 #endif
                 if (prev + nx == L.done_target)
-                    publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
+                    publish(L.ctrl, L.snap, L.seq, L.claim, kPollOf<NBLK, W0, SH, KSPAN> ? L.ctrl_next : nullptr);
             }
         } else {
             const uint32_t prev = __hip_atomic_fetch_add(&L.ctrl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1133,27 +1210,27 @@ DPOW_DEV void search_body(const Launch &L) {
                 r[2] = __builtin_amdgcn_s_memrealtime() + (prev & 0);
             }
 #endif
-            if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, kLaunchPoll<NBLK, W0, SH> ? L.ctrl_next : nullptr);
+            if (prev + 1u == L.done_target) publish(L.ctrl, L.snap, L.seq, L.claim, kPollOf<NBLK, W0, SH, KSPAN> ? L.ctrl_next : nullptr);
         }
     }
 }
 
-template <int NBLK, int W0, int SH, bool EQ>
+template <int NBLK, int W0, int SH, bool EQ, bool KSPAN>
 __global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR)))
 md5_search_kernel(const Launch L) {
-    search_body<NBLK, W0, SH, EQ>(L);
+    search_body<NBLK, W0, SH, EQ, KSPAN>(L);
 }
 
-template <int NBLK, int W0, int SH, bool EQ>
+template <int NBLK, int W0, int SH, bool EQ, bool KSPAN>
 __global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR_LONG)))
 md5_search_kernel_lsgpr(const Launch L) {
-    search_body<NBLK, W0, SH, EQ>(L);
+    search_body<NBLK, W0, SH, EQ, KSPAN>(L);
 }
 
-template <int NBLK, int W0, int SH, bool EQ>
+template <int NBLK, int W0, int SH, bool EQ, bool KSPAN>
 __global__ void __launch_bounds__(kBlockThreads) __attribute__((amdgpu_num_sgpr(DPOW_NUM_SGPR_W15)))
 md5_search_kernel_w15sgpr(const Launch L) {
-    search_body<NBLK, W0, SH, EQ>(L);
+    search_body<NBLK, W0, SH, EQ, KSPAN>(L);
 }
 
 }  // namespace DPOW_KNS

@@ -19,35 +19,42 @@ namespace dpow {
 namespace {
 using namespace DPOW_KNS;
 using KernelFn = void (*)(Launch);
-// [EQ][w0 - kW0Lo]: EQ kernels (the D-equality test, use_d_equality) exist for
-// one final block only.
+// EQ kernels (the D-equality test, use_d_equality) exist for one final block only.
 // The kernel of a layout: the long-SGPR-budget template for long nonces and two
 // final blocks (md5_search_kernel.h kLongSgpr), a slightly larger budget for the two-block
 // W0 = 15 layouts and a few more (kW15Sgpr); only the chosen one is instantiated.
-template <int NBLK, int W0, int SH, bool EQ>
+template <int NBLK, int W0, int SH, bool EQ, bool KSPAN>
 constexpr KernelFn kernel_of() {
-    if constexpr (kW15Sgpr<NBLK, W0, SH>) return md5_search_kernel_w15sgpr<NBLK, W0, SH, EQ>;
-    else if constexpr (kLongSgpr<NBLK, W0>) return md5_search_kernel_lsgpr<NBLK, W0, SH, EQ>;
-    else return md5_search_kernel<NBLK, W0, SH, EQ>;
+    if constexpr (kSgprOf<NBLK, W0, SH, KSPAN> == 2) return md5_search_kernel_w15sgpr<NBLK, W0, SH, EQ, KSPAN>;
+    else if constexpr (kSgprOf<NBLK, W0, SH, KSPAN> == 1) return md5_search_kernel_lsgpr<NBLK, W0, SH, EQ, KSPAN>;
+    else return md5_search_kernel<NBLK, W0, SH, EQ, KSPAN>;
 }
-#define DPOW_K(w, e) kernel_of<DPOW_VNBLK, w, DPOW_VSH, e>()
+// [EQ][narrow][w0 - kW0Lo]: narrow = the SH = 3 kernel without the lanes' k offset
+// (md5_search_kernel.h hash_wave_block KSPAN), for launches with R >= 64, where narrow_knobs
+// has one; other layouts have one kernel for both.
+#define DPOW_K(w, e, nar) \
+    kernel_of<DPOW_VNBLK, w, DPOW_VSH, e, !(DPOW_VSH == 3 && nar && narrow_knobs(DPOW_VNBLK, w).on)>()
 #if DPOW_VNBLK == 1
 constexpr int kW0Lo = 0;
-#define DPOW_ROW(e) \
-    {DPOW_K(0, e), DPOW_K(1, e), DPOW_K(2, e),  DPOW_K(3, e),  DPOW_K(4, e),  DPOW_K(5, e),  DPOW_K(6, e), \
-     DPOW_K(7, e), DPOW_K(8, e), DPOW_K(9, e), DPOW_K(10, e), DPOW_K(11, e), DPOW_K(12, e), DPOW_K(13, e)}
-const KernelFn kTable[2][14] = {DPOW_ROW(false), DPOW_ROW(true)};
+#define DPOW_ROW(e, n)                                                                                              \
+    {DPOW_K(0, e, n), DPOW_K(1, e, n), DPOW_K(2, e, n),  DPOW_K(3, e, n),  DPOW_K(4, e, n),  DPOW_K(5, e, n),        \
+     DPOW_K(6, e, n), DPOW_K(7, e, n), DPOW_K(8, e, n),  DPOW_K(9, e, n),  DPOW_K(10, e, n), DPOW_K(11, e, n),       \
+     DPOW_K(12, e, n), DPOW_K(13, e, n)}
+const KernelFn kTable[2][2][14] = {{DPOW_ROW(false, false), DPOW_ROW(false, true)},
+                                   {DPOW_ROW(true, false), DPOW_ROW(true, true)}};
 #else
 constexpr int kW0Lo = 12;
-#define DPOW_ROW(e) {DPOW_K(12, e), DPOW_K(13, e), DPOW_K(14, e), DPOW_K(15, e)}
-const KernelFn kTable[2][4] = {DPOW_ROW(false), DPOW_ROW(false)};
+#define DPOW_ROW(e, n) {DPOW_K(12, e, n), DPOW_K(13, e, n), DPOW_K(14, e, n), DPOW_K(15, e, n)}
+const KernelFn kTable[2][2][4] = {{DPOW_ROW(false, false), DPOW_ROW(false, true)},
+                                  {DPOW_ROW(false, false), DPOW_ROW(false, true)}};
 #endif
 #undef DPOW_ROW
 #undef DPOW_K
-constexpr int kW0N = sizeof(kTable[0]) / sizeof(kTable[0][0]);
+constexpr int kW0N = sizeof(kTable[0][0]) / sizeof(kTable[0][0][0]);
 
-KernelFn pick(int w0, bool eq) {
-    return (w0 >= kW0Lo && w0 < kW0Lo + kW0N) ? kTable[eq ? 1 : 0][w0 - kW0Lo] : nullptr;
+// narrow: the launch's R >= 64 (rbits >= 6), so no wave-block's lanes span two k
+KernelFn pick(int w0, bool eq, bool narrow) {
+    return (w0 >= kW0Lo && w0 < kW0Lo + kW0N) ? kTable[eq ? 1 : 0][narrow ? 1 : 0][w0 - kW0Lo] : nullptr;
 }
 }  // namespace
 
@@ -62,7 +69,7 @@ KernelFn pick(int w0, bool eq) {
 
 hipError_t DPOW_NAME(variant_launch_, DPOW_VNBLK, DPOW_VSH)(int w0, const Launch &L, uint32_t grid,
                                                            hipStream_t stream) {
-    KernelFn fn = pick(w0, use_d_equality(DPOW_VNBLK, L.ntz));
+    KernelFn fn = pick(w0, use_d_equality(DPOW_VNBLK, L.ntz), L.rbits >= 6u);
     if (!fn) return hipErrorInvalidValue;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlockThreads), 0, stream, L);
     return hipGetLastError();
@@ -73,17 +80,18 @@ hipError_t DPOW_NAME(variant_launch_, DPOW_VNBLK, DPOW_VSH)(int w0, const Launch
 // of its kernels: round 3's first search after dpow_open waited 972.8 us between its k = 0
 // kernel and its first md5 launch, the "_ls" unit's load (profiles/r03_final_tts_timeline.json).
 hipError_t DPOW_NAME(variant_prepare_, DPOW_VNBLK, DPOW_VSH)() {
-    for (const auto &row : kTable)
-        for (KernelFn fn : row) {
-            hipFuncAttributes a;
-            const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(fn));
-            if (e != hipSuccess) return e;
-        }
+    for (const auto &eq : kTable)
+        for (const auto &row : eq)
+            for (KernelFn fn : row) {
+                hipFuncAttributes a;
+                const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(fn));
+                if (e != hipSuccess) return e;
+            }
     return hipSuccess;
 }
 
 hipError_t DPOW_NAME(variant_occupancy_, DPOW_VNBLK, DPOW_VSH)(int w0, int *blocks_per_cu) {
-    KernelFn fn = pick(w0, false);
+    KernelFn fn = pick(w0, false, true);  // the sweep's (workerBits 0) kernel
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void *>(fn),
                                                         kBlockThreads, 0);

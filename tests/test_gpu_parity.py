@@ -378,6 +378,55 @@ def test_n8_first_hit_vs_n7_walk(miner, nlen, wbits, wb):
     assert walked >= 1
 
 
+SH3_LENGTHS = list(range(3, 64, 4)) + [67, 71, 119, 123]  # every <NBLK, W0, 3> layout, midstate too
+
+
+def test_sh3_narrow_and_general_kernels_vs_oracle(miner, oracle):
+    """SH = 3 layouts have two kernels (md5_search_kernel.h hash_wave_block KSPAN): the narrow
+    one for launches with R >= 64 (workerBits 0-2), whose word W0 + 1 is wave-uniform, and the
+    general one for R < 64, where a wave-block's lanes span several k.  Every SH = 3 layout,
+    both kernels, windows in the L = 4 and L = 5 segments and across a 2^24-k segment boundary,
+    against the oracle."""
+    rnd = random.Random(3)
+    for nlen in SH3_LENGTHS:
+        nonce = [rnd.randrange(256) for _ in range(nlen)]
+        for wbits in (0, 1, 2, 3, 5, 8):
+            wb = rnd.randrange(1 << wbits) if wbits else 0
+            rb = 8 - wbits
+            nk = (1 << 16) >> rb  # ~65k candidates per window
+            for k0 in ((1 << 24) + rnd.randrange(1 << 20), (1 << 32) + (rnd.randrange(256) << 24),
+                       (3 << 24) - nk // 2):
+                exp = oracle.mine_window(nonce, 3, wb, wbits, k0, k0 + nk)
+                r = miner.search(nonce, 3, wb, wbits, k0, k0 + nk)
+                if exp is None:
+                    assert r.status == EXHAUSTED, (nlen, wb, wbits, k0, r)
+                else:
+                    assert r.status == FOUND and r.global_idx == exp[1] and list(r.secret) == exp[0], \
+                        (nlen, wb, wbits, k0, r, exp)
+
+
+@pytest.mark.parametrize("nlen", [7, 39, 51, 59])
+def test_sh3_n9_narrow_equals_min_over_general_partitions(miner, nlen):
+    """N = 9 (the full-digest check behind the D prefilter) beyond the oracle's reach: the
+    workerBits = 0 answer of an SH = 3 layout (its narrow kernel) equals the minimum over the 8
+    partitions of workerBits = 3 (its general kernel), each searched up to that answer's k, and
+    every partition's hit verifies with hashlib (<1,1,3>, <1,9,3>, <2,12,3>, <2,14,3>)."""
+    rnd = random.Random(9000 + nlen)
+    nonce = [rnd.randrange(256) for _ in range(nlen)]
+    r0 = miner.mine(nonce, 9)
+    assert r0.status == FOUND and bytes(r0.secret) == _secret_of(r0.global_idx) and _tz(nonce, r0.secret) >= 9
+    kend = (r0.global_idx >> 8) + 1
+    gs = []
+    for wb in range(8):
+        r = miner.search(nonce, 9, wb, 3, 0, kend)
+        if r.status == FOUND:
+            assert _tz(nonce, r.secret) >= 9 and (r.global_idx & 255) >> 5 == wb, (wb, r)
+            gs.append(r.global_idx)
+        else:
+            assert r.status == EXHAUSTED, (wb, r)
+    assert min(gs) == r0.global_idx, (gs, r0.global_idx)
+
+
 def _all_hits(miner, nonce, ntz, wb, wbits, k0, k1, cap=2000):
     """Every hit of a window, in order: repeated searches resuming after each hit."""
     hits, bound_k = [], k0

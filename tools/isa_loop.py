@@ -33,8 +33,11 @@ def disasm(csrc, nblk, sh, extra):
     return subprocess.check_output([f"{LLVM}/llvm-objdump", "-d", co]).decode()
 
 
-def kernel_lines(text, nblk, w0, sh, eq=0):
-    pat = re.compile(rf"md5_search_kernel(?:_lsgpr|_w15sgpr)?ILi{nblk}ELi{w0}ELi{sh}ELb{eq}E.*>:")
+def kernel_lines(text, nblk, w0, sh, eq=0, kspan=1):
+    """kspan: the KSPAN template argument (0 = SH = 3's narrow kernel, R >= 64; every other
+    layout has only KSPAN = 1)."""
+    ks = kspan if sh == 3 else 1
+    pat = re.compile(rf"md5_search_kernel(?:_lsgpr|_w15sgpr)?ILi{nblk}ELi{w0}ELi{sh}ELb{eq}ELb{ks}E.*>:")
     out, on = [], False
     for line in text.splitlines():
         if pat.search(line):
@@ -111,13 +114,14 @@ def main():
     ap.add_argument("--sh", type=int, default=0)
     ap.add_argument("--w0", default="1,0,2,3,13")
     ap.add_argument("--eq", type=int, default=None, help="1: D-equality kernels (default for --nblk 1)")
+    ap.add_argument("--kspan", type=int, default=0, help="SH = 3: 0 = the narrow (R >= 64) kernel, 1 = the general one")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
     text = disasm(a.csrc, a.nblk, a.sh, a.extra)
     eq = (1 if a.nblk == 1 else 0) if a.eq is None else a.eq
     for w0 in [int(x) for x in a.w0.split(",")]:
-        kl = kernel_lines(text, a.nblk, w0, a.sh, eq)
+        kl = kernel_lines(text, a.nblk, w0, a.sh, eq, a.kspan)
         for lo, hi, c in hash_block_mix(kl) or []:
             valu = sum(v for k, v in c.items() if k.startswith("v_") and "lane" not in k)
             spill = c.get("v_readlane_b32", 0) + c.get("v_writelane_b32", 0)

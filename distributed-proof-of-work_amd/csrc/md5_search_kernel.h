@@ -896,7 +896,7 @@ DPOW_DEV uint64_t hash_wave_block(const Launch &L, const KConst &kc, uint64_t i0
 // SIMD, dpow_api.cpp), so a budget that still admits 7 waves costs no occupancy.
 // The short-nonce layouts keep the round-1 budget (72: no spill in the hash
 // loop; 8 waves admitted, so the next queued launch's workgroups start beside a
-// draining one).  Layouts with many launch-uniform K + M constants -- long nonces
+// draining one), except those kShort96 lists (round 6).  Layouts with many launch-uniform K + M constants -- long nonces
 // and two final blocks -- get 96: at 72 the compiler spills them to VGPR lanes
 // and reloads each with a v_readlane in every wave-block (tools/isa_loop.py:
 // 4-41 per wave-block; 0 at 96).
@@ -933,9 +933,19 @@ constexpr int kNarrowSgpr = DPOW_NSGPR > 0 ? DPOW_NSGPR : narrow_knobs(NBLK, W0)
 template <int NBLK, int W0, int SH, bool KS>
 constexpr bool kPollOf = SH == 3 && !KS && kNarrowPoll<NBLK, W0> >= 0 ? kNarrowPoll<NBLK, W0> != 0
                                                                      : kLaunchPoll<NBLK, W0, SH>;
+// Short-nonce one-block layouts (W0 <= 7, below kSgprLongW0) that take the 96 budget instead of
+// 72: every one-block kernel at 96 against the build before, per layout (round 6,
+// profiles/r06_narrow_sweep.json ab6 at workerBits 0: SH = 1-2 +0.5 to +1.5 %, SH = 0 at W0 3 and
+// 5-7 +0.8 to +1.2 %; ab5, SH = 3's general kernels at workerBits 3: W0 2-5 +0.5 to +0.9 %, W0 7
+// +6.6 %, where 72 left 7 spill reloads per wave-block).  The rest were within noise or slower
+// (<1,0,3> -3 %, <1,6,3> -3 %); the sweep kernel <1,1,0> keeps its code.  Not the "_ls" units.
+template <int NBLK, int W0, int SH, bool KS>
+constexpr bool kShort96 = NBLK == 1 && !DPOW_VLS && KS && W0 < kSgprLongW0 &&
+                          (SH == 1 || SH == 2 || (SH == 0 && (W0 == 3 || W0 >= 5)) ||
+                           (SH == 3 && ((W0 >= 2 && W0 <= 5) || W0 == 7)));
 template <int NBLK, int W0, int SH, bool KS>
 constexpr int kSgprOf = SH == 3 && !KS && kNarrowSgpr<NBLK, W0> > 0 ? kNarrowSgpr<NBLK, W0>
-                        : kW15Sgpr<NBLK, W0, SH> ? 2 : kLongSgpr<NBLK, W0> ? 1 : 0;
+                        : kW15Sgpr<NBLK, W0, SH> ? 2 : kLongSgpr<NBLK, W0> || kShort96<NBLK, W0, SH, KS> ? 1 : 0;
 
 template <int NBLK, int W0, int SH, bool EQ, bool KSPAN>
 DPOW_DEV void search_body(const Launch &L) {

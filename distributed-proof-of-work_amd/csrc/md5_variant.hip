@@ -1,7 +1,7 @@
 // md5_variant.hip -- instantiates md5_search_kernel for one (NBLK, SH) pair and
 // every word position W0 of that pair.  Compiled once per pair by the Makefile
-// (-DDPOW_VNBLK=<1|2> -DDPOW_VSH=<0..3>) so the 72 layouts (plus the 56
-// one-block D-equality kernels) build in parallel.
+// (-DDPOW_VNBLK=<1|2> -DDPOW_VSH=<0..3>) so the 72 layouts (154 kernels with the one-block
+// D-equality ones and SH = 3's narrow ones) build in parallel.
 #include "md5_search_kernel.h"
 #include "md5_variants.h"
 

@@ -6,7 +6,8 @@
 Each library runs in its own process (fresh HIP runtime, DPOW_LIB_PATH) and hashes
 2^33 candidates at N = 32 in the L = 4 segment for every nonce length 0..63 -- every
 (NBLK, W0, SH) layout -- after a full-size warm-up; two passes over the libraries,
-interleaved.  Prints one JSON object {lib: {nonce_len: [GH/s, ...]}} and the layout of
+interleaved.  DPOW_SWEEP_WBITS=b (default 0): partition 0 of workerBits b, the same
+candidate count (b >= 3 runs SH = 3's general kernels, b <= 2 its narrow ones).  Prints one JSON object {lib: {nonce_len: [GH/s, ...]}} and the layout of
 each length, from which tools/pick_leads.py chooses a per-layout build parameter.
 """
 import json
@@ -19,14 +20,15 @@ import os, sys, json
 sys.path.insert(0, os.path.join(os.environ["ROOT"], "distributed-proof-of-work_amd"))
 import torch, distpow
 K0 = 1 << 24
-NK = (1 << 33) >> 8
+WB = int(os.environ.get("DPOW_SWEEP_WBITS", "0"))
+NK = (1 << 33) >> (8 - WB)
 out = {}
 with distpow.Miner(0) as m:
-    m.search([1, 2, 3, 4], 32, 0, 0, K0, K0 + 2 * NK)
+    m.search([1, 2, 3, 4], 32, 0, WB, K0, K0 + 2 * NK)
     for n in range(64):
         nonce = [0x5A] * n
         m.reset_stats()
-        assert m.search(nonce, 32, 0, 0, K0, K0 + NK).status == distpow.EXHAUSTED
+        assert m.search(nonce, 32, 0, WB, K0, K0 + NK).status == distpow.EXHAUSTED
         st = m.stats()
         out[n] = round(st.candidates / (st.kernel_ms * 1e-3) / 1e9, 2)
 print(json.dumps(out))

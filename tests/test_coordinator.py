@@ -106,6 +106,23 @@ def test_config4_eight_workers_n8(golden, monkeypatch, split):
     assert golden_secret(golden, [2, 2, 2, 2], 8)[0] == bytes([218, 55, 128, 17])
 
 
+@pytest.mark.parametrize("W", [4, 8])
+@pytest.mark.parametrize("split", [False, True], ids=["one_gpu", "per_rank"])
+def test_sh3_nonces_both_kernels(oracle, monkeypatch, split, W):
+    """Nonces whose layout has SH = 3 (md5_search_kernel.h: a narrow kernel for R >= 64, the
+    general one for R < 64) through node mode: rank 0's workerBits-0 search (one_gpu) and the
+    per-rank partitions (per_rank: workerBits 2 narrow at W = 4, 3 general at W = 8) return the
+    oracle's workerBits = 0 first hit, from its owner alone."""
+    _split(monkeypatch, split)
+    with Coordinator(W) as c:
+        for tok, nlen in ((301, 7), (302, 31), (303, 59)):
+            nonce = [(37 * i + nlen) & 255 for i in range(nlen)]
+            sec, g, _ = oracle.mine_window(nonce, 5, 0, 0, 0, 1 << 16)
+            assert c.mine(nonce, 5, token=tok) == bytes(sec), nlen
+            check_task_protocol(c, tok, bytes(sec), g)
+        check_roles(c, split)
+
+
 @pytest.mark.parametrize("split", [False, True], ids=["one_gpu", "per_rank"])
 def test_config5_two_concurrent_clients(golden, monkeypatch, split):
     _split(monkeypatch, split)

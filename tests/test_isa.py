@@ -99,3 +99,21 @@ def test_sweep_kernel_hash_block_placement():
     assert lo % 256 == 0x68, hex(lo)
     assert sum(v for k, v in c.items() if k.startswith("v_")) == 494
 
+
+
+def test_sh3_narrow_kernels_drop_the_lane_k_adds():
+    """SH = 3's narrow kernels (launches with R >= 64: md5_search_kernel.h hash_wave_block
+    KSPAN = false) take word W0 + 1's K + M from an SGPR, so their hash block has fewer VALU
+    than the general kernel of the same layout, and neither has an SGPR spill reload in it
+    (two final blocks, every W0: DESIGN.md section 3)."""
+    import isa_loop
+    text = isa_loop.disasm(os.path.join(ROOT, "distributed-proof-of-work_amd", "csrc"), 2, 3, [])
+    for w0 in (12, 13, 14, 15):
+        valu = {}
+        for ks in (0, 1):
+            blocks = isa_loop.hash_block_mix(isa_loop.kernel_lines(text, 2, w0, 3, 0, ks))
+            assert blocks, (w0, ks)
+            lo, hi, c = max(blocks, key=lambda b: sum(b[2].values()))
+            valu[ks] = sum(v for k, v in c.items() if k.startswith("v_") and "lane" not in k)
+            assert c.get("v_readlane_b32", 0) + c.get("v_writelane_b32", 0) == 0, (w0, ks)
+        assert valu[0] + 3 <= valu[1], (w0, valu)  # 4 steps x 2 candidates of lane_k adds, less scheduling
